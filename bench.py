@@ -1,0 +1,174 @@
+"""Benchmark: Mray/s + ms/frame on bunny-in-Cornell 1920x1080 @1024spp (BASELINE.json configs[2]).
+
+One step = one full frame of the path-tracing hot path (render kernel over all pixels x spp,
+every bounce's closest-hit traversal + BSDF scatter) followed, for N > 1, by the RCCL
+all-gather of the rows to rank 0.  The frame is split into interleaved 8-row stripes across
+the N ranks (stripe s -> rank s % N), so the total work is fixed as N grows ("strong").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5] [--spp S]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  `value` = total closest-hit queries (counted in-kernel, all
+ranks) / max-over-ranks wall time of the K timed frames.  `roofline.achieved` = algorithmic
+bytes (56 B per internal-node visit + 40 B per triangle test + 20 B per sphere
+test) / render-kernel time from HIP events on the render stream.  `cpu_baseline` = the CPU
+restatement (oracle/) on the host cores, rank 0 at N = 1 only, on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # first: libpt.so then binds to the HIP runtime torch loaded
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"))
+import ptamd  # noqa: E402
+
+METRIC = "Mray/s + ms/frame, bunny-in-Cornell 1920×1080 @1024spp, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CONFIGS = {
+    "c3": ("bunny_cornell", "bunny-in-Cornell (5,000 tris) 1920x1080 @1024spp depth 50 (C3)"),
+    "c2": ("cornell", "Cornell box (32 tris) 800x800 @256spp depth 8 (C2)"),
+    "c5": ("bunny_field", "1,043,312-tri bunny field 1920x1080 @512spp depth 16 (C5)"),
+}
+STRIPE = 8
+
+
+def cpu_baseline(preset, budget_s: float = 12.0) -> dict:
+    """Oracle (scalar C++ port of the reference path, std::thread over rows) on a bounded sample:
+    the full frame at 1 spp per pass, passes repeated until `budget_s` of CPU work."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    w, h = preset.width, preset.height
+    nodes = oracle.build_lbvh(preset.objects, oracle.morton_keys(preset.objects), tight=True)
+    rows = np.arange(h, dtype=np.int32)
+    states = oracle.film_states(1, w, rows)
+    cam = ptamd.camera_to_array(preset.camera)
+    rays, passes, t0 = 0, 0, time.perf_counter()
+    while True:
+        _, st = oracle.render(preset.objects, preset.materials, nodes, cam, w, h, rows, 1, preset.max_depth,
+                              states, nthreads=threads)
+        rays += st.rays
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": rays / el / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": f"{preset.name} {w}x{h}, {passes} pass(es) of 1 spp depth {preset.max_depth} "
+                      f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel (0 = the config's)")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    name, workload = CONFIGS[args.config]
+    preset = ptamd.Preset(name)
+    spp = args.spp or preset.spp
+    w, h, depth = preset.width, preset.height, preset.max_depth
+    scene = ptamd.Scene(preset.objects, preset.materials, device=local)
+    film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
+    stripes = (h + STRIPE - 1) // STRIPE
+    max_rows = ((stripes + world - 1) // world) * STRIPE
+    local_buf = torch.zeros((max_rows * w * 3,), dtype=torch.float32, device=dev)
+    gathered = torch.empty((world * max_rows * w * 3,), dtype=torch.float32, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def frame():
+        _, st = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
+                             stream=stream.cuda_stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local_buf)
+        return st
+
+    for _ in range(args.warmup):
+        frame()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    rays = kbytes = 0
+    kms = 0.0
+    for _ in range(args.steps):
+        st = frame()
+        rays += st.rays
+        kbytes += st.algo_bytes
+        kms += st.kernel_ms
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = t[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t[1:].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, total_rays = float(mx.item()), float(sm.item())
+    else:
+        total_rays = float(rays)
+
+    if rank == 0:
+        if world > 1:   # un-permute the stripes (proves the gathered frame is complete)
+            img = torch.empty((h, w, 3), dtype=torch.float32, device=dev)
+            g = gathered.view(world, max_rows, w, 3)
+            for r in range(world):
+                rows = torch.tensor([rr for rr in range(h) if (rr // STRIPE) % world == r], device=dev)
+                img[rows] = g[r, : len(rows)]
+            torch.cuda.synchronize(dev)
+        achieved = (kbytes / 1e9) / (kms / 1e3) if kms > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": total_rays / elapsed / 1e6,
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: scene assembled from the reference's bundled OBJ models (models/), fixed seed",
+            "config": {"workload": workload, "width": w, "height": h, "spp": spp, "max_depth": depth,
+                       "stripe_rows": STRIPE, "parallelism": f"rows{world}",
+                       "rays_per_frame": total_rays / args.steps,
+                       "rng": "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "renderKernel", "kernel_ms_per_launch": kms / args.steps,
+                         "algo_bytes_per_launch": kbytes / args.steps},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(preset)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

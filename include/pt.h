@@ -1,0 +1,151 @@
+/*
+ * pt.h — C ABI of the MI355X-native path tracer (libpt.so).
+ *
+ * The reference (Nablax/Path-Tracer-CUDA-OpenGL) has no plugin/FFI layer: its boundary is
+ * the set of CUDA kernel launches and host helpers in main.cu / utils/bvh.h.  Each entry
+ * point below names the reference interface it replaces.  All functions return PT_OK (0)
+ * or a PT_ERR_* code; the message of the last failure on the calling thread is returned by
+ * pt_last_error().  No torch or HIP types appear in any signature: device pointers and
+ * streams are passed as plain pointers.
+ *
+ * Threading: one pt_scene / pt_film per device; calls on different objects may come from
+ * different threads.  There is no global mutable state besides the thread-local error.
+ */
+#ifndef PT_H
+#define PT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+enum pt_status {
+    PT_OK = 0,
+    PT_ERR_INVALID = 1,   /* bad argument */
+    PT_ERR_HIP = 2,       /* HIP runtime error (reference: checkCudaErrors, cuda_check.h:8-17) */
+    PT_ERR_IO = 3,        /* file could not be read / written */
+    PT_ERR_NOMEM = 4,
+    PT_ERR_NODEVICE = 5,  /* no GPU visible: the library never falls back to the CPU */
+    PT_ERR_STATE = 6      /* e.g. render before the BVH was built */
+};
+
+/* Object and material types: simulation/cuda_object.h:12-14, simulation/material.h:13-15 */
+enum { PT_SPHERE = 1, PT_TRIANGLE = 3 };
+enum { PT_LAMBERTIAN = 1, PT_METAL = 2, PT_DIELECTRIC = 4 };
+
+/* One scene object, the reference's CudaObj (cuda_object.h:16-123) without device pointers.
+ * sphere: v[0..2] = centre, v[3] = radius (negative radius = hollow sphere, as in RTIOW)
+ * triangle: v[0..2], v[3..5], v[6..8] = vertices v0, v1, v2 (one CudaObj per triangle). */
+typedef struct { int32_t type; int32_t mat; float v[9]; } pt_object;
+
+/* Material (material.h:17-68) in its constructed state: fuzz already clamped to <= 1. */
+typedef struct { int32_t type; float albedo[3]; float fuzz; float ir; } pt_material;
+
+/* camera (camera.h:10-76) after its host constructor ran (see pt_camera_make). */
+typedef struct {
+    float origin[3], lower_left[3], horizontal[3], vertical[3];
+    float right[3], up[3], front[3];
+    float focus_dist, lens_radius, time0, time1;
+} pt_camera;
+
+typedef struct { float o[3]; float d[3]; } pt_ray;                       /* simulation/ray.h */
+typedef struct { int32_t hit, obj, mat, front_face; float t, p[3], n[3]; } pt_hit; /* hit_record.h:12-25 */
+/* BVH node in the reference's layout (utils/bvh_node.h:8-17): internal nodes [0, n-2], root 0,
+ * leaves [n-1, 2n-2]; objid = -1 for internal nodes. */
+typedef struct { int32_t left, right, parent, objid; float bmin[3], bmax[3]; } pt_bvh_node;
+
+/* Work counters of one pt_render / pt_trace_closest call (counted in-kernel). */
+typedef struct {
+    uint64_t rays;          /* closest-hit queries: primary + every bounce */
+    uint64_t node_visits;   /* internal BVH nodes popped (each = 2 child-box tests) */
+    uint64_t box_tests;
+    uint64_t tri_tests;
+    uint64_t sphere_tests;
+    uint64_t paths;         /* camera samples */
+    double kernel_ms;       /* device time of the render/trace kernel(s), HIP events */
+    uint64_t algo_bytes;    /* 56*node_visits + 40*tri_tests + 20*sphere_tests */
+} pt_stats;
+
+/* A complete host-side scene description (objects, materials, camera, frame settings). */
+typedef struct {
+    pt_object* objects; int64_t n_objects;
+    pt_material* materials; int64_t n_materials;
+    pt_camera camera;
+    int32_t width, height, spp, max_depth;
+    char name[64];
+} pt_scene_desc;
+
+typedef struct pt_scene pt_scene;   /* device-resident objects, materials, LBVH */
+typedef struct pt_film pt_film;     /* device-resident per-pixel RNG streams for a set of rows */
+
+const char* pt_last_error(void);
+int pt_abi_version(void);
+int pt_device_count(int* count);
+
+/* ---------------------------------------------------------------- host-side surface (no GPU) */
+/* camera host ctor, camera.h:12-39 */
+int pt_camera_make(const float from[3], const float at[3], float vfov_deg, float aspect,
+                   float aperture, float focus_dist, float time0, float time1, pt_camera* out);
+/* camera::processKeyboard, camera.h:41-56 (dir: 0 FORWARD 1 BACKWARD 2 LEFT 3 RIGHT 4 UP 5 DOWN) */
+int pt_camera_move(pt_camera* cam, int dir, float delta_time);
+/* Scene builders.  name: "triangle_world" (main.cu:119-196, the reference default),
+ * "random_world" (main.cu:198-256), "test_world" (main.cu:57-117), "rtiow" (C1),
+ * "cornell" (C2), "bunny_cornell" (C3), "bunny_field" (C5).  models_dir holds
+ * cornellbox/<part>.obj and bunny/bunny.obj.  width/height <= 0 keep the preset's frame. */
+int pt_preset_scene(const char* name, const char* models_dir, int width, int height, pt_scene_desc* out);
+void pt_scene_desc_free(pt_scene_desc* desc);
+/* OBJ mesh -> triangle objects (objl::Loader::LoadFile, OBJ_Loader.hpp:426-708, flattened to
+ * one pt_object per triangle); v' = v * scale + translate.  *out is freed with pt_free. */
+int pt_load_obj(const char* path, float scale, const float translate[3], int32_t mat,
+                pt_object** out, int64_t* count);
+void pt_free(void* p);
+/* Morton keys (code << 32 | objID), stable-sorted by code: morton::computeMortonOnHost,
+ * morton_code.h:64-75.  include_origin=1 seeds the scene box with the zero box (main.cu:122). */
+int pt_morton_keys(const pt_object* objs, int64_t n, int include_origin, uint64_t* keys);
+/* PngImage::saveColor + write (png_image.h:24-37; main.cu:477-484): rgb is row-major with
+ * row 0 = bottom (as the render kernel writes it); rows are flipped on output. */
+int pt_write_png(const char* path, const float* rgb, int width, int height);
+/* Quantise exactly like saveColor: (uint8)(clamp(c, 0, 0.999) * 256), alpha 255, row flip. */
+int pt_quantize_rgba8(const float* rgb, int width, int height, uint8_t* rgba);
+
+/* ---------------------------------------------------------------- device (MI355X, gfx950) */
+/* Replaces the scene upload of generate*WorldOnHost (main.cu:173-192: cudaMalloc/cudaMemcpy,
+ * copyObjMatsToDevice, one copyTrianglesToDevice<<<1,1>>> per triangle). */
+int pt_scene_create(int device, const pt_object* objs, int64_t n_objects,
+                    const pt_material* mats, int64_t n_materials, pt_scene** out);
+/* Replaces lbvh::buildBVH (bvh.h:132-145).  flags: PT_BVH_ORIGIN_BOUNDS (default behaviour
+ * of the reference: Morton bounds contain the origin).  Internal boxes are tight. */
+#define PT_BVH_ORIGIN_BOUNDS 1
+int pt_scene_build_bvh(pt_scene* scene, int flags);
+int pt_scene_bvh_info(pt_scene* scene, int* depth, int64_t* n_nodes, int64_t* device_bytes);
+/* Download the LBVH in the reference's node layout (2n-1 nodes). */
+int pt_scene_download_bvh(pt_scene* scene, pt_bvh_node* nodes);
+/* RenderManager::hitBvh (render_manager.h:86-135) over a batch of rays, t in [tmin, tmax).
+ * rays/hits are host pointers. */
+int pt_trace_closest(pt_scene* scene, const pt_ray* rays, int64_t n, float tmin, float tmax,
+                     pt_hit* hits, pt_stats* stats);
+/* Per-pixel XORWOW streams, initRandom (main.cu:262-269): curand_init(seed, pixel, 0, ...)
+ * for every pixel of the rows this film owns.  Rows are grouped in stripes of stripe_height;
+ * stripe s belongs to part (s % n_parts).  n_parts = 1 owns the whole frame. */
+int pt_film_create(int device, int width, int height, int stripe_height, int n_parts, int part,
+                   uint64_t seed, pt_film** out);
+int pt_film_info(pt_film* film, int* n_rows, int64_t* n_pixels);
+int pt_film_rows(pt_film* film, int32_t* rows);                  /* global row of each local row */
+int pt_film_get_rng(pt_film* film, uint32_t* states);            /* n_pixels x {d, v0..v4} */
+int pt_film_set_rng(pt_film* film, const uint32_t* states);
+/* render<<<>>> (main.cu:271-294): spp samples per pixel of the film's rows, max_depth bounces.
+ * Writes sqrt(mean) RGB, 3 floats per pixel, local rows in order.  out_rgb is a device
+ * pointer when out_on_device != 0 (then `stream` is the hipStream_t to use, may be NULL),
+ * else a host pointer.  The film's RNG streams advance, as the reference's devStates do. */
+int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
+              float* out_rgb, int out_on_device, void* stream, pt_stats* stats);
+void pt_film_destroy(pt_film* film);
+void pt_scene_destroy(pt_scene* scene);   /* replaces clearWorldStates (main.cu:451-460) */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

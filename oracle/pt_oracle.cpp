@@ -1,0 +1,673 @@
+// pt_oracle.cpp — CPU restatement of the reference's hot path (TEST INFRASTRUCTURE ONLY).
+//
+// Used only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+// checker.  It is never linked into the product.  Every function cites the reference
+// file:line it restates (paths relative to the reference repository root).
+//
+// Floating point: compiled with -ffp-contract=off and no fast-math, so every expression is
+// evaluated exactly in the reference's written operation order (IEEE fp32, round to nearest).
+// The HIP kernels follow the same order, which is what makes GPU-vs-oracle images bit-exact.
+//
+// Deliberate, documented deviations from the reference:
+//  * camera lens/time draws come from the shared state[0] in the reference (main.cu:286, a
+//    cross-thread race); with aperture 0 they have no geometric effect and are skipped.
+//  * reflectance()'s powf(x, 5) (physical.h:24) is evaluated as ((x*x)*(x*x))*x.
+//  * tight internal BVH boxes (the reference seeds them with the origin, bvh.h:124-127); the
+//    reference-inflated variant is available (tight=0) to show the hits are unchanged.
+#include "pt_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include <atomic>
+
+namespace {
+
+// ---------------------------------------------------------------- vec3 (utils/vec3.h:10-104)
+struct V3 { float x, y, z; };
+inline V3 v3(float a, float b, float c) { return {a, b, c}; }
+inline V3 operator+(V3 u, V3 v) { return {u.x + v.x, u.y + v.y, u.z + v.z}; }        // :74-76
+inline V3 operator-(V3 u, V3 v) { return {u.x - v.x, u.y - v.y, u.z - v.z}; }        // :77-79
+inline V3 operator*(V3 u, V3 v) { return {u.x * v.x, u.y * v.y, u.z * v.z}; }        // :80-82
+inline V3 operator*(float t, V3 v) { return {t * v.x, t * v.y, t * v.z}; }           // :83-85
+inline V3 operator*(V3 v, float t) { return t * v; }                                  // :86-88
+inline V3 operator/(V3 v, float t) { return (1.0f / t) * v; }                         // :89-91
+inline V3 operator-(V3 v) { return {-v.x, -v.y, -v.z}; }                              // :31
+inline float dot(V3 u, V3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }            // :92-94
+inline V3 cross(V3 u, V3 v) {                                                         // :95-99
+    return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+inline float len2(V3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }               // :59
+inline V3 normalize(V3 v) {                                                           // :100-104
+    float l = std::sqrt(len2(v));
+    if (l == 0) return {0, 0, 0};
+    return v / l;
+}
+inline bool near_zero(V3 v) {                                                         // :66-69
+    const float s = 1e-7f;
+    return std::fabs(v.x) < s && std::fabs(v.y) < s && std::fabs(v.z) < s;
+}
+inline float comp(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+inline V3 load3(const float* p) { return {p[0], p[1], p[2]}; }
+inline void store3(float* p, V3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+
+struct Box { V3 mn, mx; };   // utils/aabb.h:8-51; aabb() is the zero box (vec3() zero-inits, vec3.h:13)
+
+inline Box unionBox(Box a, Box b) {                                                  // aabb.h:55-65
+    return {{std::fmin(a.mn.x, b.mn.x), std::fmin(a.mn.y, b.mn.y), std::fmin(a.mn.z, b.mn.z)},
+            {std::fmax(a.mx.x, b.mx.x), std::fmax(a.mx.y, b.mx.y), std::fmax(a.mx.z, b.mx.z)}};
+}
+
+struct Ray { V3 o, d; };
+
+// aabb::hit, aabb.h:21-34.  1/d is hoisted per ray: same value every call.
+inline bool boxHit(const float* bmin, const float* bmax, const Ray& r, V3 inv, float tmin, float tmax) {
+    for (int i = 0; i < 3; i++) {
+        float di = comp(inv, i), oi = comp(r.o, i);
+        float t0 = (bmin[i] - oi) * di;
+        float t1 = (bmax[i] - oi) * di;
+        if (di < 0.0f) std::swap(t0, t1);
+        tmin = t0 > tmin ? t0 : tmin;
+        tmax = t1 < tmax ? t1 : tmax;
+        if (tmax < tmin) return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------- objects (cuda_object.h)
+Box objectBox(const orc_object& o) {
+    if (o.type == ORC_SPHERE) {                                                       // :21-28
+        V3 c = load3(o.v);
+        float r = std::fabs(o.v[3]);
+        return {c - v3(r, r, r), c + v3(r, r, r)};
+    }
+    V3 a = load3(o.v), b = load3(o.v + 3), c = load3(o.v + 6);                        // :31-42
+    V3 mn = a, mx = a;
+    for (V3 p : {b, c}) {                                                             // aabb.h:68-79
+        if (mn.x > p.x) mn.x = p.x;
+        if (mn.y > p.y) mn.y = p.y;
+        if (mn.z > p.z) mn.z = p.z;
+        if (mx.x < p.x) mx.x = p.x;
+        if (mx.y < p.y) mx.y = p.y;
+        if (mx.z < p.z) mx.z = p.z;
+    }
+    return {mn, mx};
+}
+
+struct Hit { float t; V3 p, n; int mat, obj; bool front; };
+
+// hit_record::setFaceNormal, hit_record.h:21-24
+inline void setFaceNormal(Hit& h, const Ray& r, V3 outward) {
+    h.front = dot(r.d, outward) < 0;
+    h.n = h.front ? outward : -outward;
+}
+
+// CudaObj::hit, cuda_object.h:44-92 (getUV's output is unused and skipped).
+bool objectHit(const orc_object& o, int id, const Ray& r, float tmin, float tmax, Hit& rec, orc_stats* st) {
+    if (o.type == ORC_SPHERE) {
+        if (st) st->sphere_tests++;
+        V3 c = load3(o.v);
+        float rad = o.v[3];
+        V3 oc = r.o - c;
+        float a = len2(r.d);
+        float half_b = dot(oc, r.d);
+        float cc = len2(oc) - rad * rad;
+        float disc = half_b * half_b - a * cc;
+        if (disc < 0) return false;
+        float sq = std::sqrt(disc);
+        float root = (-half_b - sq) / a;
+        if (root < tmin || tmax < root) {
+            root = (-half_b + sq) / a;
+            if (root < tmin || tmax < root) return false;
+        }
+        rec.t = root;
+        rec.p = r.o + rec.t * r.d;                                                    // ray.h:18-20
+        V3 outward = (rec.p - c) / rad;
+        setFaceNormal(rec, r, outward);
+        rec.mat = o.mat;
+        rec.obj = id;
+        return true;
+    }
+    if (st) st->tri_tests++;
+    V3 v0 = load3(o.v), v1 = load3(o.v + 3), v2 = load3(o.v + 6);
+    V3 e1 = v1 - v0;
+    V3 e2 = v2 - v0;
+    V3 s1 = cross(r.d, e2);
+    float det = dot(s1, e1);
+    if (det == 0) return false;
+    V3 s = r.o - v0;
+    V3 s2 = cross(s, e1);
+    float inv = 1.0f / det;
+    float t = dot(s2, e2) * inv;
+    float b1 = dot(s1, s) * inv;
+    float b2 = dot(s2, r.d) * inv;
+    if (b1 >= 1 || b1 <= 0 || b2 >= 1 || b2 <= 0 || b1 + b2 <= 0 || b1 + b2 >= 1 || t <= tmin || t >= tmax)
+        return false;
+    rec.t = t;
+    rec.p = r.o + t * r.d;
+    V3 nrm = normalize(cross(v1 - v0, v2 - v0));                                      // triangle.h:17-19
+    setFaceNormal(rec, r, nrm);
+    rec.mat = o.mat;
+    rec.obj = id;
+    return true;
+}
+
+// RenderManager::hitBvh, render_manager.h:86-135 (same visiting order: left child box, right
+// child box, leaves tested immediately, internal children pushed left-then-right).
+bool hitBvh(const orc_object* objs, int64_t n, const orc_node* bvh, const Ray& r, float tmin, float tmax,
+            Hit& rec, orc_stats* st) {
+    if (n <= 0) return false;
+    float closest = tmax;
+    bool any = false;
+    Hit tmp;
+    const orc_node* cur = &bvh[0];
+    if (cur->objid != -1) {                                                           // :92-98
+        if (objectHit(objs[cur->objid], cur->objid, r, tmin, closest, tmp, st)) { any = true; rec = tmp; }
+        return any;
+    }
+    V3 inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    int stack[128];
+    int top = 0;
+    stack[top++] = 0;
+    while (top > 0) {
+        cur = &bvh[stack[--top]];
+        if (st) st->node_visits++;
+        const int kids[2] = {cur->left, cur->right};
+        for (int k = 0; k < 2; k++) {
+            const orc_node& nx = bvh[kids[k]];
+            if (st) st->box_tests++;
+            if (boxHit(nx.bmin, nx.bmax, r, inv, tmin, closest)) {
+                if (nx.objid != -1) {
+                    if (objectHit(objs[nx.objid], nx.objid, r, tmin, closest, tmp, st)) {
+                        any = true;
+                        closest = tmp.t;
+                        rec = tmp;
+                    }
+                } else {
+                    stack[top++] = kids[k];
+                }
+            }
+        }
+    }
+    return any;
+}
+
+// RenderManager::hit (brute force), render_manager.h:71-84
+bool hitBrute(const orc_object* objs, int64_t n, const Ray& r, float tmin, float tmax, Hit& rec) {
+    Hit tmp;
+    bool any = false;
+    float closest = tmax;
+    for (int64_t i = 0; i < n; i++) {
+        if (objectHit(objs[i], (int)i, r, tmin, closest, tmp, nullptr)) {
+            any = true;
+            closest = tmp.t;
+            rec = tmp;
+        }
+    }
+    return any;
+}
+
+// ---------------------------------------------------------------- XORWOW (cuRAND semantics)
+// curand_init(seed, subsequence, 0): seed scramble, then skip subsequence * 2^67 draws.
+// The xorshift part is linear over GF(2)^160; J = M^(2^67) is built by 67 squarings.
+struct Gf2Mat { uint32_t col[160][5]; };   // col[j] = image of basis vector e_j
+
+void matApply(const Gf2Mat& m, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < 160; j++)
+        if ((in[j >> 5] >> (j & 31)) & 1u)
+            for (int w = 0; w < 5; w++) r[w] ^= m.col[j][w];
+    std::memcpy(out, r, sizeof(r));
+}
+
+void xorshiftStep(uint32_t v[5]) {            // curand() body without the Weyl part
+    uint32_t t = v[0] ^ (v[0] >> 2);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+}
+
+struct JumpTables {
+    std::vector<Gf2Mat> j;   // j[k] = M^(2^(67+k))
+    JumpTables() {
+        Gf2Mat m;
+        for (int c = 0; c < 160; c++) {
+            uint32_t e[5] = {0, 0, 0, 0, 0};
+            e[c >> 5] = 1u << (c & 31);
+            xorshiftStep(e);
+            std::memcpy(m.col[c], e, sizeof(e));
+        }
+        auto square = [](const Gf2Mat& a) {
+            Gf2Mat r;
+            for (int c = 0; c < 160; c++) matApply(a, a.col[c], r.col[c]);
+            return r;
+        };
+        for (int i = 0; i < 67; i++) m = square(m);
+        j.push_back(m);
+        for (int k = 1; k < 64; k++) j.push_back(square(j.back()));
+    }
+};
+const JumpTables& jumps() {
+    static JumpTables t;
+    return t;
+}
+
+inline uint32_t xorwowNext(uint32_t s[6]) {   // curand(curandStateXORWOW*)
+    uint32_t t = s[1] ^ (s[1] >> 2);
+    s[1] = s[2]; s[2] = s[3]; s[3] = s[4]; s[4] = s[5];
+    s[5] = (s[5] ^ (s[5] << 4)) ^ (t ^ (t << 1));
+    s[0] += 362437u;
+    return s[5] + s[0];
+}
+// curand_uniform: x * 2^-32 + 2^-33, a value in (0, 1].  The product is exact (power of two),
+// so fused and unfused evaluation agree.
+inline float curandUniform(uint32_t s[6]) {
+    const float k = 2.3283064e-10f;
+    return (float)xorwowNext(s) * k + (k / 2.0f);
+}
+
+struct XorwowRng {
+    uint32_t* s;
+    float operator()() { return curandUniform(s); }
+};
+struct TapeRng {
+    const float* tape; int len; int pos;
+    float operator()() { return pos < len ? tape[pos++] : (pos++, 0.5f); }
+};
+
+// ------------------------------------------------------------ samplers (utils/utility.h)
+// vec3(curand_uniform()-0.5f, ...) arguments are drawn x, y, z in that order.
+template <class R> V3 randomOnUnitSphereDiscard(R& rng) {                              // :51-62
+    V3 res;
+    float norm;
+    do {
+        float a = rng() - 0.5f;
+        float b = rng() - 0.5f;
+        float c = rng() - 0.5f;
+        res = 2.0f * v3(a, b, c);
+        norm = len2(res);
+    } while (len2(res) >= 1.0f);
+    return res / std::sqrt(norm);
+}
+template <class R> V3 randomInUnitSphereDiscard(R& rng) {                              // :73-82
+    V3 res;
+    do {
+        float a = rng() - 0.5f;
+        float b = rng() - 0.5f;
+        float c = rng() - 0.5f;
+        res = 2.0f * v3(a, b, c);
+    } while (len2(res) >= 1.0f);
+    return res;
+}
+
+// rayphysics, physical.h:11-25
+inline V3 reflect(V3 v, V3 n) { return v - (2.0f * dot(v, n)) * n; }
+inline V3 refract(V3 uv, V3 n, float eta) {
+    float cos_theta = std::fmin(dot(-uv, n), 1.0f);
+    V3 perp = eta * (uv + cos_theta * n);
+    V3 par = (-std::sqrt(std::fabs(1.0f - len2(perp)))) * n;
+    return perp + par;
+}
+inline float reflectance(float cosine, float ref_idx) {
+    float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+    r0 = r0 * r0;
+    float x = 1.0f - cosine;
+    float x2 = x * x;
+    float x5 = (x2 * x2) * x;                 // powf(x, 5): see header note
+    return r0 + (1.0f - r0) * x5;
+}
+
+// Material::scatter, material.h:28-61
+template <class R>
+bool scatter(const orc_material& m, const Ray& in, const Hit& rec, V3& atten, Ray& out, R& rng) {
+    if (m.type == ORC_LAMBERTIAN) {
+        V3 dir = rec.n + randomOnUnitSphereDiscard(rng);
+        if (near_zero(dir)) dir = rec.n;
+        out = {rec.p, dir};
+        atten = load3(m.albedo);
+        return true;
+    }
+    if (m.type == ORC_METAL) {
+        V3 refl = reflect(normalize(in.d), rec.n);
+        V3 fz = randomInUnitSphereDiscard(rng);
+        out = {rec.p, refl + m.fuzz * fz};
+        atten = load3(m.albedo);
+        return dot(out.d, rec.n) > 0;
+    }
+    if (m.type == ORC_DIELECTRIC) {
+        atten = v3(1.0f, 1.0f, 1.0f);
+        float ratio = rec.front ? (1.0f / m.ir) : m.ir;
+        V3 ud = normalize(in.d);
+        float cos_theta = std::fmin(dot(-ud, rec.n), 1.0f);
+        float sin_theta = std::sqrt(1.0f - cos_theta * cos_theta);
+        bool cannot = (double)(ratio * sin_theta) > 1.0;
+        V3 dir;
+        if (cannot || reflectance(cos_theta, ratio) > rng())
+            dir = reflect(ud, rec.n);
+        else
+            dir = refract(ud, rec.n, ratio);
+        out = {rec.p, dir};
+        return true;
+    }
+    return false;
+}
+
+// ------------------------------------------------------------- Morton / LBVH (utils/*.h)
+uint32_t expandBits(uint32_t v) {                                                      // morton_code.h:19-27
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+uint32_t mortonCode3D(V3 c, const Box& mb) {                                           // morton_code.h:29-45
+    V3 range = mb.mx - mb.mn;
+    float x = 0, y = 0, z = 0;
+    if ((double)range.x > 1e-7) x = (c.x - mb.mn.x) / range.x;
+    if ((double)range.y > 1e-7) y = (c.y - mb.mn.y) / range.y;
+    if ((double)range.z > 1e-7) z = (c.z - mb.mn.z) / range.z;
+    x = std::fmin(std::fmax(x * 1024.0f, 0.0f), 1023.0f);
+    y = std::fmin(std::fmax(y * 1024.0f, 0.0f), 1023.0f);
+    z = std::fmin(std::fmax(z * 1024.0f, 0.0f), 1023.0f);
+    return (expandBits((uint32_t)x) << 2) + (expandBits((uint32_t)y) << 1) + expandBits((uint32_t)z);
+}
+
+inline int clz64(uint64_t x) { return x ? __builtin_clzll(x) : 64; }
+inline int delta(const uint64_t* k, int64_t n, int64_t i, int64_t j) {                 // morton_code.h:47-54
+    if (i < 0 || i >= n || j < 0 || j >= n) return -1;
+    return clz64(k[i] ^ k[j]);
+}
+inline int sgn(int x) { return (x > 0) - (x < 0); }                                    // utility.h:121-123
+
+void determineRange(const uint64_t* k, int64_t n, int64_t idx, int64_t& first, int64_t& last) {  // bvh.h:17-40
+    int ld = delta(k, n, idx, idx - 1), rd = delta(k, n, idx, idx + 1);
+    int d = sgn(rd - ld);
+    int dmin = std::min(ld, rd);
+    int64_t maxStride = 2;
+    while (delta(k, n, idx, idx + maxStride * d) > dmin) maxStride *= 2;
+    int64_t l = 0;
+    for (int64_t s = maxStride >> 1; s >= 1; s >>= 1)
+        if (delta(k, n, idx, idx + (l + s) * d) > dmin) l += s;
+    int64_t j = idx + l * d;
+    first = idx; last = j;
+    if (d < 0) std::swap(first, last);
+}
+
+int64_t findSplit(const uint64_t* k, int64_t first, int64_t last) {                   // bvh.h:42-69
+    uint64_t fc = k[first], lc = k[last];
+    if (first == last) return (first + last) >> 1;
+    int common = clz64(fc ^ lc);
+    int64_t split = first, step = last - first;
+    do {
+        step = (step + 1) >> 1;
+        int64_t ns = split + step;
+        if (ns < last) {
+            int sp = clz64(fc ^ k[ns]);
+            if (sp > common) split = ns;
+        }
+    } while (step > 1);
+    return split;
+}
+
+}  // namespace
+
+// =============================================================================== C API
+extern "C" {
+
+void orc_camera_make(const float from[3], const float at[3], float vfov, float aspect, float aperture,
+                     float focus, float t0, float t1, orc_camera* out) {              // camera.h:12-39
+    const float kDegToRad = 0.01745329252f;                                            // global_variables.h:20
+    float theta = vfov * kDegToRad;                                                    // utility.h:28-30
+    float h = std::tan(theta / 2.0f);
+    float vh = 2.0f * h;
+    float vw = aspect * vh;
+    V3 lf = load3(from), la = load3(at);
+    V3 front = normalize(lf - la);
+    V3 right = normalize(cross(v3(0, 1, 0), front));
+    V3 up = cross(front, right);
+    V3 hor = (focus * vw) * right;
+    V3 ver = (focus * vh) * up;
+    V3 ll = ((lf - hor / 2.0f) - ver / 2.0f) - focus * front;
+    store3(out->origin, lf);
+    store3(out->lower_left, ll);
+    store3(out->horizontal, hor);
+    store3(out->vertical, ver);
+    store3(out->right, right);
+    store3(out->up, up);
+    store3(out->front, front);
+    out->focus_dist = focus;
+    out->lens_radius = aperture / 2.0f;
+    out->time0 = t0;
+    out->time1 = t1;
+}
+
+void orc_xorwow_skip_subsequences(uint32_t s[6], uint64_t n) {
+    const JumpTables& jt = jumps();
+    for (int k = 0; n; k++, n >>= 1)
+        if (n & 1) matApply(jt.j[k], s + 1, s + 1);
+    // d advances by n * 2^67 * 362437 == 0 (mod 2^32): unchanged.
+}
+
+void orc_xorwow_init(uint64_t seed, uint64_t subseq, uint32_t s[6]) {
+    uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    uint32_t t0 = 1099087573u * s0;
+    uint32_t t1 = 2591861531u * s1;
+    s[0] = 6615241u + t1 + t0;
+    s[1] = 123456789u + t0;
+    s[2] = 362436069u ^ t0;
+    s[3] = 521288629u + t1;
+    s[4] = 88675123u ^ t1;
+    s[5] = 5783321u + t0;
+    orc_xorwow_skip_subsequences(s, subseq);
+}
+
+void orc_xorwow_init_range(uint64_t seed, uint64_t first, int64_t count, uint32_t* states) {
+    if (count <= 0) return;
+    uint32_t s[6];
+    orc_xorwow_init(seed, first, s);
+    const Gf2Mat& j0 = jumps().j[0];
+    for (int64_t i = 0; i < count; i++) {
+        std::memcpy(states + 6 * i, s, sizeof(s));
+        matApply(j0, s + 1, s + 1);          // subsequence i+1 = J * subsequence i
+    }
+}
+
+uint32_t orc_xorwow_next(uint32_t s[6]) { return xorwowNext(s); }
+float orc_curand_uniform(uint32_t s[6]) { return curandUniform(s); }
+
+int orc_morton_keys(const orc_object* objs, int64_t n, int include_origin, uint64_t* keys) {
+    if (n <= 0) return 0;
+    Box mb = include_origin ? Box{{0, 0, 0}, {0, 0, 0}} : objectBox(objs[0]);         // main.cu:122,166,171
+    for (int64_t i = 0; i < n; i++) mb = unionBox(mb, objectBox(objs[i]));             // aabb.h:36-44
+    std::vector<std::pair<uint32_t, uint32_t>> m(n);
+    for (int64_t i = 0; i < n; i++) {                                                  // morton_code.h:64-75
+        Box b = objectBox(objs[i]);
+        V3 c = (b.mn + b.mx) * 0.5f;                                                   // aabb.h:46-48
+        m[i] = {mortonCode3D(c, mb), (uint32_t)i};
+    }
+    std::stable_sort(m.begin(), m.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    for (int64_t i = 0; i < n; i++) keys[i] = ((uint64_t)m[i].first << 32) | m[i].second;
+    return 0;
+}
+
+int orc_build_lbvh(const orc_object* objs, int64_t n, const uint64_t* keys, int tight, orc_node* nodes) {
+    if (n <= 0) return -1;
+    const int64_t L = n - 1;                                                           // bvh.h:76
+    for (int64_t i = 0; i < 2 * n - 1; i++) {
+        nodes[i].left = nodes[i].right = nodes[i].parent = nodes[i].objid = -1;
+        for (int a = 0; a < 3; a++) nodes[i].bmin[a] = nodes[i].bmax[a] = 0.0f;
+    }
+    for (int64_t i = 0; i < n; i++) {                                                  // bvh.h:77-81
+        uint32_t id = (uint32_t)(keys[i] & 0xffffffffu);
+        Box b = objectBox(objs[id]);
+        nodes[L + i].objid = (int)id;
+        store3(nodes[L + i].bmin, b.mn);
+        store3(nodes[L + i].bmax, b.mx);
+    }
+    for (int64_t i = 0; i < n - 1; i++) {                                              // bvh.h:89-114
+        int64_t first, last;
+        determineRange(keys, n, i, first, last);
+        int64_t split = findSplit(keys, first, last);
+        int64_t a = (split == first) ? L + split : split;
+        int64_t b = (split + 1 == last) ? L + split + 1 : split + 1;
+        nodes[i].left = (int)a;
+        nodes[i].right = (int)b;
+        nodes[a].parent = (int)i;
+        nodes[b].parent = (int)i;
+    }
+    // growBBox, bvh.h:117-130, done as one correct bottom-up pass (children before parents).
+    std::vector<int> order;
+    order.reserve(n);
+    std::vector<int> pending(n > 1 ? n - 1 : 0, 2);
+    for (int64_t i = 0; i < n; i++) {
+        int p = nodes[L + i].parent;
+        while (p >= 0) {
+            if (--pending[p] > 0) break;
+            const orc_node& l = nodes[nodes[p].left];
+            const orc_node& r = nodes[nodes[p].right];
+            Box u = unionBox({load3(l.bmin), load3(l.bmax)}, {load3(r.bmin), load3(r.bmax)});
+            if (!tight) u = unionBox(Box{{0, 0, 0}, {0, 0, 0}}, u);                    // parentNode.box starts zero
+            store3(nodes[p].bmin, u.mn);
+            store3(nodes[p].bmax, u.mx);
+            p = nodes[p].parent;
+        }
+    }
+    return 0;
+}
+
+int orc_bvh_depth(const orc_node* nodes, int64_t n) {
+    if (n <= 1) return 0;
+    int best = 0;
+    std::vector<std::pair<int, int>> st{{0, 1}};
+    while (!st.empty()) {
+        auto [i, d] = st.back();
+        st.pop_back();
+        best = std::max(best, d);
+        for (int c : {nodes[i].left, nodes[i].right})
+            if (nodes[c].objid == -1) st.push_back({c, d + 1});
+    }
+    return best;
+}
+
+int orc_trace(const orc_object* objs, int64_t nobj, const orc_node* nodes, const float* rays, int64_t nrays,
+              float tmin, float tmax, int brute, orc_hit* hits, orc_stats* stats) {
+    for (int64_t i = 0; i < nrays; i++) {
+        Ray r{load3(rays + 6 * i), load3(rays + 6 * i + 3)};
+        Hit h;
+        bool ok = brute ? hitBrute(objs, nobj, r, tmin, tmax, h) : hitBvh(objs, nobj, nodes, r, tmin, tmax, h, stats);
+        if (stats) stats->rays++;
+        orc_hit& o = hits[i];
+        std::memset(&o, 0, sizeof(o));
+        o.hit = ok ? 1 : 0;
+        o.obj = ok ? h.obj : -1;
+        o.mat = ok ? h.mat : -1;
+        if (ok) {
+            o.front_face = h.front ? 1 : 0;
+            o.t = h.t;
+            store3(o.p, h.p);
+            store3(o.n, h.n);
+        }
+    }
+    return 0;
+}
+
+int orc_scatter_tape(const orc_material* m, const float ray[6], const orc_hit* rec, const float* tape, int tape_len,
+                     int* used, float out_ray[6], float atten[3]) {
+    TapeRng rng{tape, tape_len, 0};
+    Hit h;
+    h.t = rec->t;
+    h.p = load3(rec->p);
+    h.n = load3(rec->n);
+    h.front = rec->front_face != 0;
+    h.mat = rec->mat;
+    h.obj = rec->obj;
+    Ray in{load3(ray), load3(ray + 3)}, out{{0, 0, 0}, {0, 0, 0}};
+    V3 a{0, 0, 0};
+    bool ok = scatter(*m, in, h, a, out, rng);
+    if (used) *used = rng.pos;
+    store3(out_ray, out.o);
+    store3(out_ray + 3, out.d);
+    store3(atten, a);
+    return ok ? 1 : 0;
+}
+
+int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
+               const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
+               uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads) {
+    (void)nmat; (void)height;
+    if (nthreads < 1) nthreads = 1;
+    const V3 pos = load3(cam->origin), ll = load3(cam->lower_left);
+    const V3 hor = load3(cam->horizontal), ver = load3(cam->vertical);
+    const float invW = 1.0f / (float)width, invH = 1.0f / (float)height, invSpp = 1.0f / (float)spp;  // main.cu:281
+    std::atomic<int> next{0};
+    std::mutex mu;
+    auto worker = [&]() {
+        orc_stats local{};
+        for (;;) {
+            int ri = next.fetch_add(1);
+            if (ri >= nrows) break;
+            const int row = rows[ri];
+            for (int col = 0; col < width; col++) {
+                const int64_t k = (int64_t)ri * width + col;
+                uint32_t* s = states + 6 * k;
+                XorwowRng rng{s};
+                V3 sum{0, 0, 0};
+                for (int i = 0; i < spp; i++) {                                        // main.cu:283-289
+                    float u = ((float)col + curandUniform(s)) * invW;
+                    float v = ((float)row + curandUniform(s)) * invH;
+                    Ray r{pos, ((ll + u * hor) + v * ver) - pos};                      // camera.h:58-64
+                    local.paths++;
+                    // rayTracing, main.cu:21-37
+                    V3 att{1, 1, 1};
+                    Ray cur = r;
+                    int depth = max_depth;
+                    V3 c;
+                    bool absorbed = false;
+                    while (depth-- > 0) {
+                        Hit rec;
+                        local.rays++;
+                        if (!hitBvh(objs, nobj, nodes, cur, 0.001f, std::numeric_limits<float>::infinity(), rec, &local))
+                            break;
+                        V3 na;
+                        Ray sc;
+                        if (!scatter(mats[rec.mat], cur, rec, na, sc, rng)) { absorbed = true; break; }
+                        att = att * na;                                                 // vec3::operator*=
+                        cur = sc;
+                    }
+                    if (absorbed) {
+                        c = {0, 0, 0};
+                    } else {
+                        V3 ud = normalize(cur.d);
+                        float t = 0.5f * (ud.y + 1.0f);
+                        c = ((1.0f - t) * v3(1.0f, 1.0f, 1.0f) + t * v3(0.5f, 0.7f, 1.0f)) * att;
+                    }
+                    sum = sum + c;                                                      // vec3::operator+=
+                }
+                out_rgb[3 * k + 0] = std::sqrt(sum.x * invSpp);                        // main.cu:290-293
+                out_rgb[3 * k + 1] = std::sqrt(sum.y * invSpp);
+                out_rgb[3 * k + 2] = std::sqrt(sum.z * invSpp);
+            }
+        }
+        if (stats) {
+            std::lock_guard<std::mutex> g(mu);
+            stats->rays += local.rays;
+            stats->node_visits += local.node_visits;
+            stats->box_tests += local.box_tests;
+            stats->tri_tests += local.tri_tests;
+            stats->sphere_tests += local.sphere_tests;
+            stats->paths += local.paths;
+        }
+    };
+    (void)jumps();
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; t++) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+    return 0;
+}
+
+}  // extern "C"

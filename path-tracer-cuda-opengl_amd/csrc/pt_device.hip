@@ -1,0 +1,1112 @@
+// pt_device.hip — MI355X (gfx950) device path: LBVH build, closest-hit traversal, render.
+//
+// Hot path re-designed for CDNA4:
+//  * render: one lane per pixel of an 8x8 tile (one wave per workgroup), path regeneration
+//    (a lane whose path ends starts its next sample in the same loop iteration, so no lane
+//    idles between samples), per-lane XORWOW state in registers, coalesced SoA state I/O.
+//  * traversal: BVH2 whose internal-node record holds BOTH child boxes + child refs (64 B,
+//    four dwordx4 loads per visit, one 64-B segment); leaves are folded into the parent's
+//    child refs; the traversal stack lives in LDS, lane-interleaved (conflict-free).
+//  * primitives are stored in Morton (leaf) order, 48 B each; normals separately (fetched
+//    once per closest hit, not per test).
+//  * LBVH: Karras hierarchy kernel + atomic-counter bottom-up refit with tight boxes.
+// All arithmetic follows the reference's operation order and is compiled with
+// -ffp-contract=off, so results are bit-identical to oracle/ (the CPU restatement).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../host/pt_error.hpp"
+#include "../host/pt_host.hpp"
+#include "pt.h"
+
+using pt::fail;
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            return fail(PT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kSphereBit = 0x40000000u;
+constexpr uint32_t kPrimMask = 0x3fffffffu;
+constexpr int kJumpMats = 32;                    // XORWOW 2^(67+k) jump matrices, k < 32
+
+// ------------------------------------------------------------------------ device structs
+struct DevScene {
+    const float4* nodes;     // 4 x float4 per internal node: lmin.xyz lmax.x | lmax.yz rmin.xy | rmin.z rmax.xyz | refs
+    const float4* prims;     // 3 x float4 per primitive (leaf order)
+    const float4* normals;   // 1 x float4 per primitive (triangles)
+    const float4* mats;      // 2 x float4 per material
+    unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
+    int nprims;
+};
+
+struct DevCamera {
+    float3 pos, ll, hor, ver;
+};
+
+struct Counters {
+    uint32_t rays, visits, tris, spheres;
+};
+
+// ------------------------------------------------------------------------ math helpers
+// Exact restatements of utils/vec3.h operators (no contraction: -ffp-contract=off).
+__device__ __forceinline__ float3 f3(float a, float b, float c) { return make_float3(a, b, c); }
+__device__ __forceinline__ float3 add(float3 a, float3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ float3 sub(float3 a, float3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ float3 mul(float3 a, float3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ float3 scale(float t, float3 v) { return f3(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ float3 neg(float3 v) { return f3(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot3(float3 a, float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float3 cross3(float3 u, float3 v) {
+    return f3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
+}
+__device__ __forceinline__ float len2(float3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
+__device__ __forceinline__ float3 divs(float3 v, float t) { return scale(1.0f / t, v); }
+__device__ __forceinline__ float3 normalize3(float3 v) {
+    float l = sqrtf(len2(v));
+    if (l == 0.0f) return f3(0.0f, 0.0f, 0.0f);
+    return divs(v, l);
+}
+__device__ __forceinline__ float3 xyz(float4 v) { return f3(v.x, v.y, v.z); }
+
+// ------------------------------------------------------------------------ XORWOW
+struct Xorwow {
+    uint32_t d, v0, v1, v2, v3, v4;
+    __device__ __forceinline__ uint32_t next() {   // curand(curandStateXORWOW*)
+        uint32_t t = v0 ^ (v0 >> 2);
+        v0 = v1; v1 = v2; v2 = v3; v3 = v4;
+        v4 = (v4 ^ (v4 << 4)) ^ (t ^ (t << 1));
+        d += 362437u;
+        return v4 + d;
+    }
+    // curand_uniform: x * 2^-32 + 2^-33 in (0, 1]
+    __device__ __forceinline__ float uniform() { return (float)next() * 0x1p-32f + 0x1p-33f; }
+};
+
+// ------------------------------------------------------------------------ traversal
+// aabb::hit (aabb.h:21-34): per axis t0=(min-o)*inv, t1=(max-o)*inv, swap if inv<0,
+// tmin=max(tmin,t0), tmax=min(tmax,t1); miss if tmax<tmin.  The ternaries of the reference
+// keep the old bound on NaN, which is exactly maxNum/minNum (v_max_f32 / v_min_f32).
+__device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                     float3 o, float3 inv, float tmin, float tmax) {
+    float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
+    float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
+    float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
+    float nx = inv.x < 0.0f ? t1x : t0x, fx = inv.x < 0.0f ? t0x : t1x;
+    float ny = inv.y < 0.0f ? t1y : t0y, fy = inv.y < 0.0f ? t0y : t1y;
+    float nz = inv.z < 0.0f ? t1z : t0z, fz = inv.z < 0.0f ? t0z : t1z;
+    float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
+    float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
+    return !(hi < lo);
+}
+
+// CudaObj::hit (cuda_object.h:44-92) for the primitive in leaf slot `ref`; on acceptance
+// updates closest/best.  Triangle edges e1 = v1-v0, e2 = v2-v0 are precomputed (same values).
+__device__ __forceinline__ void primTest(const DevScene& S, uint32_t ref, float3 o, float3 d, float tmin,
+                                         float& closest, int& best, Counters& c) {
+    const uint32_t k = ref & kPrimMask;
+    const float4* p = S.prims + 3 * (size_t)k;
+    if (ref & kSphereBit) {
+        c.spheres++;
+        float4 p0 = p[0], p1 = p[1];
+        float3 oc = sub(o, xyz(p0));
+        float r = p1.x;
+        float a = len2(d);
+        float half_b = dot3(oc, d);
+        float cc = len2(oc) - r * r;
+        float disc = half_b * half_b - a * cc;
+        if (disc < 0.0f) return;
+        float sq = sqrtf(disc);
+        float root = (-half_b - sq) / a;
+        if (root < tmin || closest < root) {
+            root = (-half_b + sq) / a;
+            if (root < tmin || closest < root) return;
+        }
+        closest = root;
+        best = (int)k;
+    } else {
+        c.tris++;
+        float4 p0 = p[0], p1 = p[1], p2 = p[2];
+        float3 e1 = xyz(p1), e2 = xyz(p2);
+        float3 s1 = cross3(d, e2);
+        float det = dot3(s1, e1);
+        if (det == 0.0f) return;
+        float3 s = sub(o, xyz(p0));
+        float3 s2 = cross3(s, e1);
+        float inv = 1.0f / det;
+        float t = dot3(s2, e2) * inv;
+        float b1 = dot3(s1, s) * inv;
+        float b2 = dot3(s2, d) * inv;
+        if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 <= 0.0f || b1 + b2 >= 1.0f ||
+            t <= tmin || t >= closest)
+            return;
+        closest = t;
+        best = (int)k;
+    }
+}
+
+// RenderManager::hitBvh (render_manager.h:86-135): same visiting order (left child, right
+// child, leaf children tested at once, internal children pushed left then right).
+// Returns the leaf slot of the closest hit or -1; `closest` holds its t.
+template <int STACK>
+__device__ __forceinline__ int trace(const DevScene& S, float3 o, float3 d, float tmin, float& closest,
+                                     uint32_t* stk, Counters& c) {
+    int best = -1;
+    if (S.nprims <= 0) return -1;
+    if (S.nprims == 1) {   // root is a leaf: tested without a box test (:92-98)
+        const uint32_t ref = kLeafBit | (__float_as_uint(S.prims[2].w) ? kSphereBit : 0u);
+        primTest(S, ref, o, d, tmin, closest, best, c);
+        return best;
+    }
+    const float3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int node = 0, sp = 0, guard = 0;
+    for (;;) {
+        // Each internal node is visited at most once per query; more means a corrupt tree.
+        if (++guard > S.nprims) { atomicOr(S.err, 1u); break; }
+        c.visits++;
+        const float4* np = S.nodes + 4 * (size_t)node;
+        const float4 a = np[0], b = np[1], q = np[2], r = np[3];
+        const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
+        if (slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, closest)) {
+            if (lref & kLeafBit) primTest(S, lref, o, d, tmin, closest, best, c);
+            else if (sp < STACK) { stk[sp * kWave] = lref; sp++; }
+            else { atomicOr(S.err, 2u); break; }
+        }
+        if (slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, tmin, closest)) {
+            if (rref & kLeafBit) primTest(S, rref, o, d, tmin, closest, best, c);
+            else if (sp < STACK) { stk[sp * kWave] = rref; sp++; }
+            else { atomicOr(S.err, 2u); break; }
+        }
+        if (sp == 0) break;
+        sp--;
+        node = (int)stk[sp * kWave];
+    }
+    return best;
+}
+
+// Hit record for leaf slot k at distance t (cuda_object.h:62-67 / 85-88, hit_record.h:21-24).
+struct HitRec { float3 p, n; int mat, obj; bool front; };
+
+__device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, float3 o, float3 d) {
+    HitRec h;
+    const float4* p = S.prims + 3 * (size_t)k;
+    const float4 p0 = p[0], p1 = p[1];
+    h.p = add(o, scale(t, d));
+    float3 outward;
+    if (__float_as_uint(p[2].w)) {   // sphere
+        outward = divs(sub(h.p, xyz(p0)), p1.x);
+    } else {
+        outward = xyz(S.normals[k]);
+    }
+    h.front = dot3(d, outward) < 0.0f;
+    h.n = h.front ? outward : neg(outward);
+    h.mat = (int)__float_as_uint(p0.w);
+    h.obj = (int)__float_as_uint(p1.w);
+    return h;
+}
+
+// ------------------------------------------------------------------------ BSDFs
+// utility.h:51-62 / 73-82; vec3(...) arguments drawn x, y, z in order.
+__device__ __forceinline__ float3 onUnitSphere(Xorwow& g) {
+    float3 res;
+    float norm;
+    do {
+        float a = g.uniform() - 0.5f;
+        float b = g.uniform() - 0.5f;
+        float cz = g.uniform() - 0.5f;
+        res = scale(2.0f, f3(a, b, cz));
+        norm = len2(res);
+    } while (norm >= 1.0f);
+    return divs(res, sqrtf(norm));
+}
+__device__ __forceinline__ float3 inUnitSphere(Xorwow& g) {
+    float3 res;
+    do {
+        float a = g.uniform() - 0.5f;
+        float b = g.uniform() - 0.5f;
+        float cz = g.uniform() - 0.5f;
+        res = scale(2.0f, f3(a, b, cz));
+    } while (len2(res) >= 1.0f);
+    return res;
+}
+__device__ __forceinline__ float3 reflect3(float3 v, float3 n) { return sub(v, scale(2.0f * dot3(v, n), n)); }
+
+// Material::scatter (material.h:28-61); returns false when the path is absorbed.
+__device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, float3& d, float3& atten, Xorwow& g) {
+    const float4 m0 = S.mats[2 * h.mat], m1 = S.mats[2 * h.mat + 1];
+    const int type = (int)__float_as_uint(m1.y);
+    if (type == PT_LAMBERTIAN) {
+        float3 dir = add(h.n, onUnitSphere(g));
+        if (fabsf(dir.x) < 1e-7f && fabsf(dir.y) < 1e-7f && fabsf(dir.z) < 1e-7f) dir = h.n;
+        d = dir;
+        atten = xyz(m0);
+        return true;
+    }
+    if (type == PT_METAL) {
+        float3 refl = reflect3(normalize3(d), h.n);
+        float3 fz = inUnitSphere(g);
+        d = add(refl, scale(m0.w, fz));
+        atten = xyz(m0);
+        return dot3(d, h.n) > 0.0f;
+    }
+    if (type == PT_DIELECTRIC) {
+        atten = f3(1.0f, 1.0f, 1.0f);
+        const float ir = m1.x;
+        float ratio = h.front ? (1.0f / ir) : ir;
+        float3 ud = normalize3(d);
+        float cos_t = fminf(dot3(neg(ud), h.n), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        bool cannot = ratio * sin_t > 1.0f;
+        bool refl = cannot;
+        if (!cannot) {   // reflectance (physical.h:20-25), pow(x,5) = ((x*x)*(x*x))*x
+            float r0 = (1.0f - ratio) / (1.0f + ratio);
+            r0 = r0 * r0;
+            float x = 1.0f - cos_t;
+            float x2 = x * x;
+            float rf = r0 + (1.0f - r0) * ((x2 * x2) * x);
+            refl = rf > g.uniform();
+        }
+        if (refl) {
+            d = reflect3(ud, h.n);
+        } else {   // refract (physical.h:14-19)
+            float ct = fminf(dot3(neg(ud), h.n), 1.0f);
+            float3 perp = scale(ratio, add(ud, scale(ct, h.n)));
+            float3 par = scale(-sqrtf(fabsf(1.0f - len2(perp))), h.n);
+            d = add(perp, par);
+        }
+        return true;
+    }
+    return false;
+}
+
+// Sky (main.cu:34-36) times attenuation.
+__device__ __forceinline__ float3 sky(float3 d, float3 att) {
+    float3 ud = normalize3(d);
+    float t = 0.5f * (ud.y + 1.0f);
+    float3 c = add(scale(1.0f - t, f3(1.0f, 1.0f, 1.0f)), scale(t, f3(0.5f, 0.7f, 1.0f)));
+    return mul(c, att);
+}
+
+// ------------------------------------------------------------------------ kernels
+struct RenderParams {
+    DevScene S;
+    DevCamera cam;
+    uint32_t *sd, *s0, *s1, *s2, *s3, *s4;   // film RNG state, SoA over local pixels
+    float* out;
+    unsigned long long* counters;             // rays, visits, tris, spheres, paths
+    int width, nrows, stripe_h, nparts, part;
+    int tiles_x, ntiles;
+    int spp, max_depth;
+    float invW, invH, invSpp;
+};
+
+__device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
+    return ((lrow / sh) * nparts + part) * sh + lrow % sh;
+}
+
+// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so
+// give each XCD a contiguous band of tiles (its L2 then holds one band's working set).
+// Bijective: XCD x (= bid % 8) owns q + (x < r) tiles starting at x*q + min(x, r).
+__device__ __forceinline__ int xcdTile(int bid, int ntiles) {
+    const int q = ntiles >> 3, r = ntiles & 7, x = bid & 7;
+    return x * q + min(x, r) + (bid >> 3);
+}
+
+__device__ __forceinline__ void waveReduceAdd(unsigned long long* dst, uint32_t v) {
+    unsigned long long x = v;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0 && x) atomicAdd(dst, x);
+}
+
+template <int STACK>
+__global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    const int tile = xcdTile(blockIdx.x, P.ntiles);
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int col = tx * 8 + (lane & 7);
+    const int lrow = ty * 8 + (lane >> 3);
+    const bool valid = col < P.width && lrow < P.nrows;
+    Counters c{0, 0, 0, 0};
+    uint32_t paths = 0;
+    if (valid) {
+        const size_t idx = (size_t)lrow * P.width + col;
+        const int row = globalRow(lrow, P.stripe_h, P.nparts, P.part);
+        Xorwow g{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+        const float fcol = (float)col, frow = (float)row;
+        float3 sum = f3(0.0f, 0.0f, 0.0f);
+        float3 o, d, att;
+        int depthLeft = 0, sample = 0;
+        // newPath: main.cu:284-286 + camera::get_ray (camera.h:58-64), lens/time draws skipped.
+        auto newPath = [&]() {
+            float u = (fcol + g.uniform()) * P.invW;
+            float v = (frow + g.uniform()) * P.invH;
+            o = P.cam.pos;
+            d = sub(add(add(P.cam.ll, scale(u, P.cam.hor)), scale(v, P.cam.ver)), P.cam.pos);
+            att = f3(1.0f, 1.0f, 1.0f);
+            depthLeft = P.max_depth;
+            paths++;
+        };
+        if (P.max_depth <= 0) {
+            for (; sample < P.spp; sample++) { newPath(); sum = add(sum, sky(d, att)); }
+        } else if (P.spp > 0) {
+            newPath();
+            uint32_t* my = stk + lane;
+            for (;;) {
+                // one bounce of rayTracing (main.cu:26-33) for this lane's current path
+                c.rays++;
+                depthLeft--;
+                float closest = __builtin_inff();
+                const int k = trace<STACK>(P.S, o, d, 0.001f, closest, my, c);
+                bool done = false;
+                float3 contrib;
+                if (k < 0) {
+                    contrib = sky(d, att);
+                    done = true;
+                } else {
+                    HitRec h = makeHit(P.S, k, closest, o, d);
+                    float3 na;
+                    if (!scatter(P.S, h, d, na, g)) {
+                        contrib = f3(0.0f, 0.0f, 0.0f);
+                        done = true;
+                    } else {
+                        att = mul(att, na);
+                        o = h.p;
+                        if (depthLeft == 0) { contrib = sky(d, att); done = true; }
+                    }
+                }
+                if (done) {
+                    sum = add(sum, contrib);
+                    if (++sample == P.spp) break;
+                    newPath();
+                }
+            }
+        }
+        float* outp = P.out + 3 * idx;   // main.cu:290-293
+        outp[0] = sqrtf(sum.x * P.invSpp);
+        outp[1] = sqrtf(sum.y * P.invSpp);
+        outp[2] = sqrtf(sum.z * P.invSpp);
+        P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+    }
+    waveReduceAdd(P.counters + 0, c.rays);
+    waveReduceAdd(P.counters + 1, c.visits);
+    waveReduceAdd(P.counters + 2, c.tris);
+    waveReduceAdd(P.counters + 3, c.spheres);
+    waveReduceAdd(P.counters + 4, paths);
+}
+
+template <int STACK>
+__global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* rays, int64_t n, float tmin,
+                                                     float tmax, pt_hit* hits, unsigned long long* counters) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kWave + lane;
+    Counters c{0, 0, 0, 0};
+    if (i < n) {
+        const pt_ray r = rays[i];
+        const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
+        float closest = tmax;
+        c.rays++;
+        const int k = trace<STACK>(S, o, d, tmin, closest, stk + lane, c);
+        pt_hit h = {};
+        h.obj = -1;
+        h.mat = -1;
+        if (k >= 0) {
+            HitRec hr = makeHit(S, k, closest, o, d);
+            h.hit = 1;
+            h.obj = hr.obj;
+            h.mat = hr.mat;
+            h.front_face = hr.front ? 1 : 0;
+            h.t = closest;
+            h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
+            h.n[0] = hr.n.x; h.n[1] = hr.n.y; h.n[2] = hr.n.z;
+        }
+        hits[i] = h;
+    }
+    waveReduceAdd(counters + 0, c.rays);
+    waveReduceAdd(counters + 1, c.visits);
+    waveReduceAdd(counters + 2, c.tris);
+    waveReduceAdd(counters + 3, c.spheres);
+}
+
+// initRandom (main.cu:262-269): curand_init(seed, pixel, 0).  The subsequence skip is the
+// GF(2) product of jump matrices J_k = M^(2^(67+k)) for the set bits of the pixel index.
+// Loops are wave-uniform (k, j); column loads are uniform, hence scalar.
+__global__ __launch_bounds__(256) void rngInitKernel(uint32_t* sd, uint32_t* s0, uint32_t* s1, uint32_t* s2,
+                                                     uint32_t* s3, uint32_t* s4, const uint32_t* __restrict__ jm,
+                                                     uint64_t seed, int width, int nrows, int sh, int nparts,
+                                                     int part) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t npix = (int64_t)width * nrows;
+    if (idx >= npix) return;
+    const int lrow = (int)(idx / width), col = (int)(idx % width);
+    const uint64_t pixel = (uint64_t)globalRow(lrow, sh, nparts, part) * (uint64_t)width + (uint64_t)col;
+    const uint32_t a = (uint32_t)seed ^ 0xaad26b49u, b = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * a, t1 = 2591861531u * b;
+    uint32_t v[5] = {123456789u + t0, 362436069u ^ t0, 521288629u + t1, 88675123u ^ t1, 5783321u + t0};
+    const uint32_t d = 6615241u + t1 + t0;
+    for (int k = 0; k < kJumpMats; k++) {
+        if (!((pixel >> k) & 1u)) continue;
+        const uint32_t* m = jm + (size_t)k * 160 * 5;
+        uint32_t r[5] = {0, 0, 0, 0, 0};
+        for (int j = 0; j < 160; j++) {
+            const uint32_t bit = (v[j >> 5] >> (j & 31)) & 1u;
+            const uint32_t mask = 0u - bit;
+#pragma unroll
+            for (int w = 0; w < 5; w++) r[w] ^= m[j * 5 + w] & mask;
+        }
+#pragma unroll
+        for (int w = 0; w < 5; w++) v[w] = r[w];
+    }
+    sd[idx] = d; s0[idx] = v[0]; s1[idx] = v[1]; s2[idx] = v[2]; s3[idx] = v[3]; s4[idx] = v[4];
+}
+
+// --- LBVH (utils/bvh.h:17-130) -----------------------------------------------------------
+__device__ __forceinline__ int deltaK(const unsigned long long* k, long long n, long long i, long long j) {   // morton_code.h:47-54
+    if (i < 0 || i >= n || j < 0 || j >= n) return -1;
+    return __clzll(k[i] ^ k[j]);
+}
+
+// generateLBVH (bvh.h:71-115) with the node reset separated from the linking (no race):
+// writes child refs of internal node i and the parent link of both children.
+__global__ void karrasKernel(const unsigned long long* __restrict__ keys, int n, float4* nodes, int* iparent,
+                             int* lparent, const uint32_t* __restrict__ leafSphere) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    // determineRange (bvh.h:17-40)
+    const int ld = deltaK(keys, n, i, i - 1), rd = deltaK(keys, n, i, i + 1);
+    const int dir = (rd - ld > 0) - (rd - ld < 0);
+    const int dmin = min(ld, rd);
+    long long maxStride = 2;
+    while (deltaK(keys, n, i, i + maxStride * dir) > dmin) maxStride *= 2;
+    long long l = 0;
+    for (long long s = maxStride >> 1; s >= 1; s >>= 1)
+        if (deltaK(keys, n, i, i + (l + s) * dir) > dmin) l += s;
+    int first = i, last = (int)(i + l * dir);
+    if (dir < 0) { int t = first; first = last; last = t; }
+    // findSplit (bvh.h:42-69)
+    const unsigned long long fc = keys[first], lc = keys[last];
+    int split;
+    if (first == last) {
+        split = (first + last) >> 1;
+    } else {
+        const int common = __clzll(fc ^ lc);
+        split = first;
+        int step = last - first;
+        do {
+            step = (step + 1) >> 1;
+            const int ns = split + step;
+            if (ns < last && __clzll(fc ^ keys[ns]) > common) split = ns;
+        } while (step > 1);
+    }
+    uint32_t a, b;
+    if (split == first) { a = kLeafBit | (leafSphere[split] ? kSphereBit : 0u) | (uint32_t)split; lparent[split] = i; }
+    else { a = (uint32_t)split; iparent[split] = i; }
+    if (split + 1 == last) { b = kLeafBit | (leafSphere[split + 1] ? kSphereBit : 0u) | (uint32_t)(split + 1); lparent[split + 1] = i; }
+    else { b = (uint32_t)(split + 1); iparent[split + 1] = i; }
+    nodes[4 * (size_t)i + 3] = make_float4(__uint_as_float(a), __uint_as_float(b), 0.0f, 0.0f);
+}
+
+// Writes a child box into slot (0 = left, 1 = right) of node p with write-through stores.
+__device__ __forceinline__ void storeBox(float4* nodes, int p, int slot, const float b[6]) {
+    float* f = reinterpret_cast<float*>(nodes + 4 * (size_t)p) + slot * 6;
+#pragma unroll
+    for (int i = 0; i < 6; i++) __hip_atomic_store(f + i, b[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void loadBox(const float4* nodes, int p, int slot, float b[6]) {
+    const float* f = reinterpret_cast<const float*>(nodes + 4 * (size_t)p) + slot * 6;
+#pragma unroll
+    for (int i = 0; i < 6; i++) b[i] = __hip_atomic_load(f + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// growBBox (bvh.h:117-130) as a correct bottom-up refit: every leaf writes its box into its
+// parent's slot, then climbs; the second thread to reach a node (agent-scope acq_rel counter)
+// unions the node's two child boxes into the grandparent's slot.  Tight boxes.
+__global__ void refitKernel(float4* nodes, const int* __restrict__ iparent, const int* __restrict__ lparent,
+                            const float* __restrict__ leafBoxes, unsigned int* arrivals, int n) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    float b[6];
+    for (int i = 0; i < 6; i++) b[i] = leafBoxes[6 * (size_t)k + i];
+    int p = lparent[k];
+    uint32_t childRef = kLeafBit;   // compare on the index bits only
+    int self = k;
+    bool leaf = true;
+    for (int guard = 0; p >= 0 && guard < 130; guard++) {
+        const float4 refs = nodes[4 * (size_t)p + 3];
+        const uint32_t lref = __float_as_uint(refs.x);
+        const bool isLeft = leaf ? ((lref & kLeafBit) && (int)(lref & kPrimMask) == self)
+                                 : (!(lref & kLeafBit) && (int)lref == self);
+        storeBox(nodes, p, isLeft ? 0 : 1, b);
+        const unsigned int prev =
+            __hip_atomic_fetch_add(arrivals + p, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == 0) return;   // sibling not done yet: it will carry on
+        float l6[6], r6[6];
+        loadBox(nodes, p, 0, l6);
+        loadBox(nodes, p, 1, r6);
+        for (int i = 0; i < 3; i++) {   // utils::unionBox (aabb.h:55-65)
+            b[i] = fminf(l6[i], r6[i]);
+            b[3 + i] = fmaxf(l6[3 + i], r6[3 + i]);
+        }
+        self = p;
+        leaf = false;
+        p = iparent[p];
+    }
+    (void)childRef;
+}
+
+// ------------------------------------------------------------------------ host helpers
+// GF(2) 160x160 jump matrices for XORWOW's xorshift part (product-side implementation).
+struct Mat160 { uint32_t c[160][5]; };
+
+void apply160(const Mat160& m, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < 160; j++) {
+        const uint32_t mask = 0u - ((in[j / 32] >> (j % 32)) & 1u);
+        for (int w = 0; w < 5; w++) r[w] ^= m.c[j][w] & mask;
+    }
+    std::memcpy(out, r, sizeof(r));
+}
+
+const std::vector<uint32_t>& jumpMatrices() {
+    static const std::vector<uint32_t> tables = [] {
+        Mat160 m;
+        for (int j = 0; j < 160; j++) {   // image of basis vector e_j under one xorshift step
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[j / 32] = 1u << (j % 32);
+            const uint32_t t = v[0] ^ (v[0] >> 2);
+            const uint32_t nv[5] = {v[1], v[2], v[3], v[4], (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1))};
+            std::memcpy(m.c[j], nv, sizeof(nv));
+        }
+        auto sq = [](const Mat160& a) {
+            Mat160 r;
+            for (int j = 0; j < 160; j++) apply160(a, a.c[j], r.c[j]);
+            return r;
+        };
+        for (int i = 0; i < 67; i++) m = sq(m);
+        std::vector<uint32_t> out((size_t)kJumpMats * 160 * 5);
+        for (int k = 0; k < kJumpMats; k++) {
+            std::memcpy(&out[(size_t)k * 800], m.c, sizeof(m.c));
+            m = sq(m);
+        }
+        return out;
+    }();
+    return tables;
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+int devAlloc(DevBuf& b, size_t bytes) {
+    if (b.p) { (void)hipFree(b.p); b.p = nullptr; }
+    if (bytes == 0) bytes = 16;
+    HIP_TRY(hipMalloc(&b.p, bytes));
+    return PT_OK;
+}
+
+int stackFor(int depth) {
+    const int need = depth + 1;
+    for (int s : {16, 32, 48, 64, 80})
+        if (need <= s) return s;
+    return -1;
+}
+
+}  // namespace
+
+// ================================================================== opaque objects
+struct pt_scene {
+    int device = 0;
+    int64_t nobj = 0, nmat = 0;
+    std::vector<pt_object> objs;            // host copy (BVH build input)
+    DevBuf mats, nodes, prims, normals, counters;
+    std::vector<uint64_t> keys;             // sorted Morton keys of the current BVH
+    std::vector<int32_t> iparent, lparent;  // host copies for download
+    std::vector<float> leafBoxes;           // 6 floats per leaf slot
+    int depth = 0;
+    bool built = false;
+    size_t deviceBytes = 0;
+};
+
+struct pt_film {
+    int device = 0;
+    int width = 0, height = 0, stripe_h = 1, nparts = 1, part = 0;
+    int nrows = 0;
+    int64_t npix = 0;
+    DevBuf state;   // 6 x npix uint32 (SoA)
+};
+
+namespace {
+int setDevice(int dev) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(PT_ERR_NODEVICE, "no HIP device visible (the library has no CPU fallback)");
+    if (dev < 0 || dev >= count) return fail(PT_ERR_INVALID, "device index out of range");
+    HIP_TRY(hipSetDevice(dev));
+    return PT_OK;
+}
+
+template <int S>
+void launchRender(const RenderParams& P, hipStream_t st) {
+    renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
+}
+int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
+    switch (stack) {
+        case 16: launchRender<16>(P, st); break;
+        case 32: launchRender<32>(P, st); break;
+        case 48: launchRender<48>(P, st); break;
+        case 64: launchRender<64>(P, st); break;
+        case 80: launchRender<80>(P, st); break;
+        default: return fail(PT_ERR_STATE, "unsupported BVH depth");
+    }
+    HIP_TRY(hipGetLastError());
+    return PT_OK;
+}
+int dispatchTrace(int stack, const DevScene& S, const pt_ray* r, int64_t n, float tmin, float tmax, pt_hit* h,
+                  unsigned long long* cnt, hipStream_t st) {
+    const unsigned blocks = (unsigned)((n + kWave - 1) / kWave);
+    switch (stack) {
+        case 16: traceKernel<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+        case 32: traceKernel<32><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+        case 48: traceKernel<48><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+        case 64: traceKernel<64><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+        case 80: traceKernel<80><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+        default: return fail(PT_ERR_STATE, "unsupported BVH depth");
+    }
+    HIP_TRY(hipGetLastError());
+    return PT_OK;
+}
+
+DevScene devScene(const pt_scene* s) {
+    DevScene S;
+    S.nodes = s->nodes.as<float4>();
+    S.prims = s->prims.as<float4>();
+    S.normals = s->normals.as<float4>();
+    S.mats = s->mats.as<float4>();
+    S.err = reinterpret_cast<unsigned int*>(s->counters.as<unsigned long long>() + 7);
+    S.nprims = (int)s->nobj;
+    return S;
+}
+
+void fillStats(pt_stats* st, const unsigned long long c[5], double ms) {
+    if (!st) return;
+    std::memset(st, 0, sizeof(*st));
+    st->rays = c[0];
+    st->node_visits = c[1];
+    st->box_tests = 2 * c[1];
+    st->tri_tests = c[2];
+    st->sphere_tests = c[3];
+    st->paths = c[4];
+    st->kernel_ms = ms;
+    st->algo_bytes = 56ull * c[1] + 40ull * c[2] + 20ull * c[3];
+}
+}  // namespace
+
+// ================================================================== C ABI (device part)
+extern "C" {
+
+int pt_device_count(int* count) {
+    if (!count) return fail(PT_ERR_INVALID, "pt_device_count: null");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return PT_OK;
+}
+
+int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_material* mats, int64_t nmat,
+                    pt_scene** out) {
+    if (!out || n < 0 || nmat < 0 || (n > 0 && !objs) || (nmat > 0 && !mats))
+        return fail(PT_ERR_INVALID, "pt_scene_create: bad argument");
+    if (n >= (int64_t)kPrimMask) return fail(PT_ERR_INVALID, "pt_scene_create: too many objects");
+    for (int64_t i = 0; i < n; i++) {
+        if (objs[i].type != PT_SPHERE && objs[i].type != PT_TRIANGLE)
+            return fail(PT_ERR_INVALID, "pt_scene_create: unknown object type");
+        if (objs[i].mat < 0 || objs[i].mat >= nmat) return fail(PT_ERR_INVALID, "pt_scene_create: material id out of range");
+    }
+    int rc = setDevice(device);
+    if (rc) return rc;
+    std::unique_ptr<pt_scene> s(new pt_scene);
+    s->device = device;
+    s->nobj = n;
+    s->nmat = nmat;
+    s->objs.assign(objs, objs + n);
+    // materials: (albedo.xyz, fuzz), (ir, type, 0, 0)
+    std::vector<float4> m((size_t)std::max<int64_t>(1, 2 * nmat));
+    for (int64_t i = 0; i < nmat; i++) {
+        m[2 * i] = make_float4(mats[i].albedo[0], mats[i].albedo[1], mats[i].albedo[2], mats[i].fuzz);
+        uint32_t t = (uint32_t)mats[i].type;
+        float tf;
+        std::memcpy(&tf, &t, 4);
+        m[2 * i + 1] = make_float4(mats[i].ir, tf, 0.0f, 0.0f);
+    }
+    if ((rc = devAlloc(s->mats, m.size() * sizeof(float4)))) return rc;
+    HIP_TRY(hipMemcpy(s->mats.p, m.data(), m.size() * sizeof(float4), hipMemcpyHostToDevice));
+    if ((rc = devAlloc(s->counters, 8 * sizeof(unsigned long long)))) return rc;
+    *out = s.release();
+    return PT_OK;
+}
+
+int pt_scene_build_bvh(pt_scene* s, int flags) {
+    if (!s) return fail(PT_ERR_INVALID, "pt_scene_build_bvh: null scene");
+    int rc = setDevice(s->device);
+    if (rc) return rc;
+    const int64_t n = s->nobj;
+    s->built = false;
+    s->keys.assign((size_t)n, 0);
+    if (n > 0) pt::mortonKeys(s->objs.data(), n, (flags & PT_BVH_ORIGIN_BOUNDS) != 0, s->keys.data());
+    // primitives in leaf order: (v0|c, mat) (e1|r, obj) (e2, isSphere); leaf boxes (cuda_object.h:21-42)
+    std::vector<float4> prims((size_t)std::max<int64_t>(1, 3 * n)), normals((size_t)std::max<int64_t>(1, n));
+    std::vector<float> boxes((size_t)std::max<int64_t>(1, 6 * n));
+    std::vector<uint32_t> sphereFlag((size_t)std::max<int64_t>(1, n));
+    auto bits = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
+    for (int64_t k = 0; k < n; k++) {
+        const uint32_t id = (uint32_t)(s->keys[k] & 0xffffffffu);
+        const pt_object& o = s->objs[id];
+        float* bx = &boxes[6 * k];
+        if (o.type == PT_SPHERE) {
+            prims[3 * k] = make_float4(o.v[0], o.v[1], o.v[2], bits((uint32_t)o.mat));
+            prims[3 * k + 1] = make_float4(o.v[3], 0.0f, 0.0f, bits(id));
+            prims[3 * k + 2] = make_float4(0.0f, 0.0f, 0.0f, bits(1u));
+            normals[k] = make_float4(0, 0, 0, 0);
+            const float r = std::fabs(o.v[3]);
+            for (int a = 0; a < 3; a++) { bx[a] = o.v[a] - r; bx[3 + a] = o.v[a] + r; }
+            sphereFlag[k] = 1;
+        } else {
+            const pt::vec3 v0(o.v[0], o.v[1], o.v[2]), v1(o.v[3], o.v[4], o.v[5]), v2(o.v[6], o.v[7], o.v[8]);
+            const pt::vec3 e1 = v1 - v0, e2 = v2 - v0;
+            const pt::vec3 nn = pt::normalize(pt::cross(v1 - v0, v2 - v0));   // triangle.h:17-19
+            prims[3 * k] = make_float4(v0.x(), v0.y(), v0.z(), bits((uint32_t)o.mat));
+            prims[3 * k + 1] = make_float4(e1.x(), e1.y(), e1.z(), bits(id));
+            prims[3 * k + 2] = make_float4(e2.x(), e2.y(), e2.z(), bits(0u));
+            normals[k] = make_float4(nn.x(), nn.y(), nn.z(), 0.0f);
+            for (int a = 0; a < 3; a++) {
+                float mn = o.v[a], mx = o.v[a];
+                for (int q = 1; q < 3; q++) {
+                    if (mn > o.v[3 * q + a]) mn = o.v[3 * q + a];
+                    if (mx < o.v[3 * q + a]) mx = o.v[3 * q + a];
+                }
+                bx[a] = mn;
+                bx[3 + a] = mx;
+            }
+            sphereFlag[k] = 0;
+        }
+    }
+    s->leafBoxes = boxes;
+    const int64_t ni = std::max<int64_t>(0, n - 1);
+    if ((rc = devAlloc(s->prims, prims.size() * sizeof(float4)))) return rc;
+    if ((rc = devAlloc(s->normals, normals.size() * sizeof(float4)))) return rc;
+    if ((rc = devAlloc(s->nodes, (size_t)std::max<int64_t>(1, ni) * 4 * sizeof(float4)))) return rc;
+    HIP_TRY(hipMemcpy(s->prims.p, prims.data(), prims.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->normals.p, normals.data(), normals.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(s->nodes.p, 0, (size_t)std::max<int64_t>(1, ni) * 4 * sizeof(float4)));
+    s->iparent.assign((size_t)std::max<int64_t>(1, ni), -1);
+    s->lparent.assign((size_t)std::max<int64_t>(1, n), -1);
+    s->depth = 0;
+    if (n > 1) {
+        DevBuf dkeys, dip, dlp, dbox, darr, dsph;
+        if ((rc = devAlloc(dkeys, n * 8)) || (rc = devAlloc(dip, ni * 4)) || (rc = devAlloc(dlp, n * 4)) ||
+            (rc = devAlloc(dbox, n * 24)) || (rc = devAlloc(darr, ni * 4)) || (rc = devAlloc(dsph, n * 4)))
+            return rc;
+        HIP_TRY(hipMemcpy(dkeys.p, s->keys.data(), n * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(dbox.p, boxes.data(), n * 24, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(dsph.p, sphereFlag.data(), n * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(dip.p, 0xff, ni * 4));
+        HIP_TRY(hipMemset(dlp.p, 0xff, n * 4));
+        HIP_TRY(hipMemset(darr.p, 0, ni * 4));
+        const int tb = 256;
+        karrasKernel<<<(unsigned)((ni + tb - 1) / tb), tb>>>(dkeys.as<unsigned long long>(), (int)n,
+                                                                s->nodes.as<float4>(), dip.as<int>(), dlp.as<int>(),
+                                                                dsph.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+        refitKernel<<<(unsigned)((n + tb - 1) / tb), tb>>>(s->nodes.as<float4>(), dip.as<int>(), dlp.as<int>(),
+                                                             dbox.as<float>(), darr.as<unsigned int>(), (int)n);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(s->iparent.data(), dip.p, ni * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(s->lparent.data(), dlp.p, n * 4, hipMemcpyDeviceToHost));
+        // depth of the internal hierarchy (root = 1): picks the LDS stack size
+        std::vector<int> d((size_t)ni, 0);
+        std::vector<float4> tmp((size_t)ni * 4);
+        HIP_TRY(hipMemcpy(tmp.data(), s->nodes.p, ni * 4 * sizeof(float4), hipMemcpyDeviceToHost));
+        d[0] = 1;
+        int maxd = 1;
+        std::vector<int> st{0};
+        while (!st.empty()) {
+            int i = st.back();
+            st.pop_back();
+            for (float f : {tmp[4 * i + 3].x, tmp[4 * i + 3].y}) {
+                uint32_t r;
+                std::memcpy(&r, &f, 4);
+                if (!(r & kLeafBit)) {
+                    d[r] = d[i] + 1;
+                    maxd = std::max(maxd, d[r]);
+                    st.push_back((int)r);
+                }
+            }
+        }
+        s->depth = maxd;
+    }
+    if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
+    s->deviceBytes = (size_t)ni * 64 + (size_t)n * 64 + (size_t)s->nmat * 32;
+    s->built = true;
+    return PT_OK;
+}
+
+int pt_scene_bvh_info(pt_scene* s, int* depth, int64_t* nodes, int64_t* bytes) {
+    if (!s) return fail(PT_ERR_INVALID, "pt_scene_bvh_info: null scene");
+    if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
+    if (depth) *depth = s->depth;
+    if (nodes) *nodes = s->nobj > 0 ? 2 * s->nobj - 1 : 0;
+    if (bytes) *bytes = (int64_t)s->deviceBytes;
+    return PT_OK;
+}
+
+int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
+    if (!s || !out) return fail(PT_ERR_INVALID, "pt_scene_download_bvh: null argument");
+    if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
+    int rc = setDevice(s->device);
+    if (rc) return rc;
+    const int64_t n = s->nobj;
+    if (n <= 0) return PT_OK;
+    const int64_t L = n - 1;
+    std::vector<float4> nodes((size_t)std::max<int64_t>(1, L) * 4), prims((size_t)n * 3);
+    if (L > 0) HIP_TRY(hipMemcpy(nodes.data(), s->nodes.p, L * 4 * sizeof(float4), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < 2 * n - 1; i++) {
+        out[i].left = out[i].right = out[i].parent = out[i].objid = -1;
+        for (int a = 0; a < 3; a++) out[i].bmin[a] = out[i].bmax[a] = 0.0f;
+    }
+    auto refIndex = [&](uint32_t r) -> int64_t { return (r & kLeafBit) ? L + (int64_t)(r & kPrimMask) : (int64_t)r; };
+    for (int64_t k = 0; k < n; k++) {
+        out[L + k].objid = (int32_t)(s->keys[k] & 0xffffffffu);
+        out[L + k].parent = L > 0 ? s->lparent[k] : -1;
+    }
+    for (int64_t i = 0; i < L; i++) {
+        const float* f = reinterpret_cast<const float*>(&nodes[4 * i]);
+        uint32_t lr, rr;
+        std::memcpy(&lr, f + 12, 4);
+        std::memcpy(&rr, f + 13, 4);
+        out[i].left = (int32_t)refIndex(lr);
+        out[i].right = (int32_t)refIndex(rr);
+        out[i].parent = i == 0 ? -1 : s->iparent[i];
+        for (int c = 0; c < 2; c++) {   // child boxes live in this record; copy them to the child
+            pt_bvh_node& ch = out[c == 0 ? out[i].left : out[i].right];
+            for (int a = 0; a < 3; a++) { ch.bmin[a] = f[6 * c + a]; ch.bmax[a] = f[6 * c + 3 + a]; }
+        }
+        if (i == 0) {   // the root's own box (never tested by the traversal)
+            for (int a = 0; a < 3; a++) {
+                out[0].bmin[a] = std::fmin(f[a], f[6 + a]);
+                out[0].bmax[a] = std::fmax(f[3 + a], f[9 + a]);
+            }
+        }
+    }
+    if (L == 0) {   // single object: the root is the leaf (bvh.h:76-81 with numObjects = 1)
+        for (int a = 0; a < 3; a++) { out[0].bmin[a] = s->leafBoxes[a]; out[0].bmax[a] = s->leafBoxes[3 + a]; }
+    }
+    return PT_OK;
+}
+
+int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, float tmax, pt_hit* hits,
+                     pt_stats* stats) {
+    if (!s || n < 0 || (n > 0 && (!rays || !hits))) return fail(PT_ERR_INVALID, "pt_trace_closest: bad argument");
+    if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
+    int rc = setDevice(s->device);
+    if (rc) return rc;
+    const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
+    DevBuf dr, dh;
+    if ((rc = devAlloc(dr, n * sizeof(pt_ray))) || (rc = devAlloc(dh, n * sizeof(pt_hit)))) return rc;
+    if (n > 0) HIP_TRY(hipMemcpy(dr.p, rays, n * sizeof(pt_ray), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(s->counters.p, 0, 8 * sizeof(unsigned long long)));
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, 0));
+    if (n > 0 && (rc = dispatchTrace(stack, devScene(s), dr.as<pt_ray>(), n, tmin, tmax, dh.as<pt_hit>(),
+                                     s->counters.as<unsigned long long>(), 0))) {
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(e1, 0));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (n > 0) HIP_TRY(hipMemcpy(hits, dh.p, n * sizeof(pt_hit), hipMemcpyDeviceToHost));
+    unsigned long long c[8] = {0};
+    HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
+    c[4] = 0;
+    fillStats(stats, c, ms);
+    if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
+    return PT_OK;
+}
+
+int pt_film_create(int device, int width, int height, int sh, int nparts, int part, uint64_t seed, pt_film** out) {
+    if (!out || width <= 0 || height <= 0 || sh <= 0 || nparts <= 0 || part < 0 || part >= nparts)
+        return fail(PT_ERR_INVALID, "pt_film_create: bad argument");
+    if ((int64_t)width * height >= (1ll << kJumpMats)) return fail(PT_ERR_INVALID, "pt_film_create: frame too large");
+    int rc = setDevice(device);
+    if (rc) return rc;
+    std::unique_ptr<pt_film> f(new pt_film);
+    f->device = device;
+    f->width = width;
+    f->height = height;
+    f->stripe_h = sh;
+    f->nparts = nparts;
+    f->part = part;
+    int rows = 0;
+    for (int r = 0; r < height; r++)
+        if ((r / sh) % nparts == part) rows++;
+    f->nrows = rows;
+    f->npix = (int64_t)rows * width;
+    if ((rc = devAlloc(f->state, (size_t)std::max<int64_t>(1, f->npix) * 6 * 4))) return rc;
+    if (f->npix > 0) {
+        const std::vector<uint32_t>& jm = jumpMatrices();
+        DevBuf djm;
+        if ((rc = devAlloc(djm, jm.size() * 4))) return rc;
+        HIP_TRY(hipMemcpy(djm.p, jm.data(), jm.size() * 4, hipMemcpyHostToDevice));
+        uint32_t* b = f->state.as<uint32_t>();
+        const int64_t np = f->npix;
+        rngInitKernel<<<(unsigned)((np + 255) / 256), 256>>>(b, b + np, b + 2 * np, b + 3 * np, b + 4 * np, b + 5 * np,
+                                                               djm.as<uint32_t>(), seed, width, rows, sh, nparts, part);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    *out = f.release();
+    return PT_OK;
+}
+
+int pt_film_info(pt_film* f, int* nrows, int64_t* npix) {
+    if (!f) return fail(PT_ERR_INVALID, "pt_film_info: null film");
+    if (nrows) *nrows = f->nrows;
+    if (npix) *npix = f->npix;
+    return PT_OK;
+}
+
+int pt_film_rows(pt_film* f, int32_t* rows) {
+    if (!f || !rows) return fail(PT_ERR_INVALID, "pt_film_rows: null argument");
+    int k = 0;
+    for (int r = 0; r < f->height; r++)
+        if ((r / f->stripe_h) % f->nparts == f->part) rows[k++] = r;
+    return PT_OK;
+}
+
+int pt_film_get_rng(pt_film* f, uint32_t* states) {
+    if (!f || !states) return fail(PT_ERR_INVALID, "pt_film_get_rng: null argument");
+    int rc = setDevice(f->device);
+    if (rc) return rc;
+    const int64_t np = f->npix;
+    std::vector<uint32_t> soa((size_t)np * 6);
+    if (np) HIP_TRY(hipMemcpy(soa.data(), f->state.p, np * 24, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < np; i++)
+        for (int w = 0; w < 6; w++) states[6 * i + w] = soa[(size_t)w * np + i];
+    return PT_OK;
+}
+
+int pt_film_set_rng(pt_film* f, const uint32_t* states) {
+    if (!f || !states) return fail(PT_ERR_INVALID, "pt_film_set_rng: null argument");
+    int rc = setDevice(f->device);
+    if (rc) return rc;
+    const int64_t np = f->npix;
+    std::vector<uint32_t> soa((size_t)np * 6);
+    for (int64_t i = 0; i < np; i++)
+        for (int w = 0; w < 6; w++) soa[(size_t)w * np + i] = states[6 * i + w];
+    if (np) HIP_TRY(hipMemcpy(f->state.p, soa.data(), np * 24, hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+int pt_render(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_depth, float* out, int on_dev,
+              void* stream, pt_stats* stats) {
+    if (!s || !f || !cam || !out || spp <= 0) return fail(PT_ERR_INVALID, "pt_render: bad argument");
+    if (!s->built) return fail(PT_ERR_STATE, "pt_render: BVH not built");
+    if (s->device != f->device) return fail(PT_ERR_INVALID, "pt_render: scene and film on different devices");
+    if (cam->lens_radius != 0.0f)
+        return fail(PT_ERR_INVALID, "pt_render: aperture > 0 is not supported (reference draws the lens sample "
+                                    "from a shared racy stream, main.cu:286)");
+    int rc = setDevice(s->device);
+    if (rc) return rc;
+    hipStream_t st = on_dev ? (hipStream_t)stream : 0;
+    const int64_t np = f->npix;
+    DevBuf dout;
+    float* dst = out;
+    if (!on_dev) {
+        if ((rc = devAlloc(dout, (size_t)std::max<int64_t>(1, np) * 12))) return rc;
+        dst = dout.as<float>();
+    }
+    HIP_TRY(hipMemsetAsync(s->counters.p, 0, 8 * sizeof(unsigned long long), st));
+    RenderParams P;
+    P.S = devScene(s);
+    P.cam.pos = make_float3(cam->origin[0], cam->origin[1], cam->origin[2]);
+    P.cam.ll = make_float3(cam->lower_left[0], cam->lower_left[1], cam->lower_left[2]);
+    P.cam.hor = make_float3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
+    P.cam.ver = make_float3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
+    uint32_t* b = f->state.as<uint32_t>();
+    P.sd = b; P.s0 = b + np; P.s1 = b + 2 * np; P.s2 = b + 3 * np; P.s3 = b + 4 * np; P.s4 = b + 5 * np;
+    P.out = dst;
+    P.counters = s->counters.as<unsigned long long>();
+    P.width = f->width;
+    P.nrows = f->nrows;
+    P.stripe_h = f->stripe_h;
+    P.nparts = f->nparts;
+    P.part = f->part;
+    P.tiles_x = (f->width + 7) / 8;
+    P.ntiles = P.tiles_x * ((f->nrows + 7) / 8);
+    P.spp = spp;
+    P.max_depth = max_depth;
+    P.invW = 1.0f / (float)f->width;    // main.cu:281
+    P.invH = 1.0f / (float)f->height;
+    P.invSpp = 1.0f / (float)spp;
+    const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+    if (P.ntiles > 0 && (rc = dispatchRender(stack, P, st))) {
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * 12, hipMemcpyDeviceToHost));
+    unsigned long long c[8] = {0};
+    HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
+    fillStats(stats, c, ms);
+    if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
+    return PT_OK;
+}
+
+void pt_film_destroy(pt_film* f) {
+    if (!f) return;
+    (void)hipSetDevice(f->device);
+    delete f;
+}
+
+void pt_scene_destroy(pt_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    delete s;
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+"""ptamd — ctypes binding of libpt.so (include/pt.h) for tests, smoke() and bench.py.
+
+This module only marshals arguments: every computation happens in libpt.so (host C++ for
+scene assembly / PNG, HIP kernels for the LBVH build, traversal and render).  There is no
+CPU fallback: if libpt.so is missing, importing this module raises; if no GPU is visible,
+device calls fail with PT_ERR_NODEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libpt.so")
+MODELS_DIR = os.path.join(REPO, "models")
+
+PT_OK = 0
+PT_SPHERE, PT_TRIANGLE = 1, 3
+PT_LAMBERTIAN, PT_METAL, PT_DIELECTRIC = 1, 2, 4
+PT_BVH_ORIGIN_BOUNDS = 1
+
+# numpy mirrors of the C structs (all 4-byte fields, no padding)
+OBJECT_DTYPE = np.dtype([("type", "<i4"), ("mat", "<i4"), ("v", "<f4", (9,))])
+MATERIAL_DTYPE = np.dtype([("type", "<i4"), ("albedo", "<f4", (3,)), ("fuzz", "<f4"), ("ir", "<f4")])
+RAY_DTYPE = np.dtype([("o", "<f4", (3,)), ("d", "<f4", (3,))])
+HIT_DTYPE = np.dtype([("hit", "<i4"), ("obj", "<i4"), ("mat", "<i4"), ("front_face", "<i4"),
+                      ("t", "<f4"), ("p", "<f4", (3,)), ("n", "<f4", (3,))])
+NODE_DTYPE = np.dtype([("left", "<i4"), ("right", "<i4"), ("parent", "<i4"), ("objid", "<i4"),
+                       ("bmin", "<f4", (3,)), ("bmax", "<f4", (3,))])
+assert OBJECT_DTYPE.itemsize == 44 and MATERIAL_DTYPE.itemsize == 24 and HIT_DTYPE.itemsize == 44
+
+
+class Camera(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("lower_left", C.c_float * 3), ("horizontal", C.c_float * 3),
+                ("vertical", C.c_float * 3), ("right", C.c_float * 3), ("up", C.c_float * 3),
+                ("front", C.c_float * 3), ("focus_dist", C.c_float), ("lens_radius", C.c_float),
+                ("time0", C.c_float), ("time1", C.c_float)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("box_tests", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("paths", C.c_uint64),
+                ("kernel_ms", C.c_double), ("algo_bytes", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("objects", C.c_void_p), ("n_objects", C.c_int64), ("materials", C.c_void_p),
+                ("n_materials", C.c_int64), ("camera", Camera), ("width", C.c_int32), ("height", C.c_int32),
+                ("spp", C.c_int32), ("max_depth", C.c_int32), ("name", C.c_char * 64)]
+
+
+# Every symbol include/pt.h declares (checked by the CPU tests).
+EXPORTS = [
+    "pt_last_error", "pt_abi_version", "pt_device_count", "pt_camera_make", "pt_camera_move",
+    "pt_preset_scene", "pt_scene_desc_free", "pt_load_obj", "pt_free", "pt_morton_keys", "pt_write_png",
+    "pt_quantize_rgba8", "pt_scene_create", "pt_scene_build_bvh", "pt_scene_bvh_info", "pt_scene_download_bvh",
+    "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
+    "pt_render", "pt_film_destroy", "pt_scene_destroy",
+]
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} not built (run `make -C path-tracer-cuda-opengl_amd` or __graft_entry__.build())")
+lib = C.CDLL(LIB_PATH)
+
+_P = C.c_void_p
+_sig = {
+    "pt_last_error": (C.c_char_p, []),
+    "pt_abi_version": (C.c_int, []),
+    "pt_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "pt_camera_make": (C.c_int, [_P, _P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
+                                 C.POINTER(Camera)]),
+    "pt_camera_move": (C.c_int, [C.POINTER(Camera), C.c_int, C.c_float]),
+    "pt_preset_scene": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(SceneDesc)]),
+    "pt_scene_desc_free": (None, [C.POINTER(SceneDesc)]),
+    "pt_load_obj": (C.c_int, [C.c_char_p, C.c_float, _P, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
+    "pt_free": (None, [_P]),
+    "pt_morton_keys": (C.c_int, [_P, C.c_int64, C.c_int, _P]),
+    "pt_write_png": (C.c_int, [C.c_char_p, _P, C.c_int, C.c_int]),
+    "pt_quantize_rgba8": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+    "pt_scene_create": (C.c_int, [C.c_int, _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_void_p)]),
+    "pt_scene_build_bvh": (C.c_int, [_P, C.c_int]),
+    "pt_scene_bvh_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "pt_scene_download_bvh": (C.c_int, [_P, _P]),
+    "pt_trace_closest": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, _P, C.POINTER(Stats)]),
+    "pt_film_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                 C.POINTER(C.c_void_p)]),
+    "pt_film_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
+    "pt_film_rows": (C.c_int, [_P, _P]),
+    "pt_film_get_rng": (C.c_int, [_P, _P]),
+    "pt_film_set_rng": (C.c_int, [_P, _P]),
+    "pt_render": (C.c_int, [_P, _P, C.POINTER(Camera), C.c_int, C.c_int, _P, C.c_int, _P, C.POINTER(Stats)]),
+    "pt_film_destroy": (None, [_P]),
+    "pt_scene_destroy": (None, [_P]),
+}
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+class PtError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        msg = lib.pt_last_error().decode(errors="replace")
+        super().__init__(f"{where} failed with status {code}: {msg}")
+        self.code = code
+
+
+def _check(rc: int, where: str) -> None:
+    if rc != PT_OK:
+        raise PtError(rc, where)
+
+
+def _ptr(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(lib.pt_device_count(C.byref(n)), "pt_device_count")
+    return n.value
+
+
+def camera_make(frm, at, vfov, aspect, aperture=0.0, focus=10.0, t0=0.0, t1=1.0) -> Camera:
+    cam = Camera()
+    f = np.asarray(frm, np.float32)
+    a = np.asarray(at, np.float32)
+    _check(lib.pt_camera_make(_ptr(f), _ptr(a), vfov, aspect, aperture, focus, t0, t1, C.byref(cam)), "pt_camera_make")
+    return cam
+
+
+def camera_to_array(cam: Camera) -> np.ndarray:
+    return np.frombuffer(bytes(cam), dtype=np.float32).copy()
+
+
+class Preset:
+    """Host-side scene description produced by pt_preset_scene."""
+
+    def __init__(self, name: str, width: int = 0, height: int = 0, models_dir: str = MODELS_DIR):
+        d = SceneDesc()
+        _check(lib.pt_preset_scene(name.encode(), models_dir.encode(), width, height, C.byref(d)), "pt_preset_scene")
+        try:
+            ob = (C.c_char * (d.n_objects * OBJECT_DTYPE.itemsize)).from_address(d.objects) if d.n_objects else b""
+            mb = (C.c_char * (d.n_materials * MATERIAL_DTYPE.itemsize)).from_address(d.materials) if d.n_materials else b""
+            self.objects = np.frombuffer(bytes(ob), dtype=OBJECT_DTYPE).copy()
+            self.materials = np.frombuffer(bytes(mb), dtype=MATERIAL_DTYPE).copy()
+            self.camera = Camera.from_buffer_copy(bytes(d.camera))
+            self.width, self.height, self.spp, self.max_depth = d.width, d.height, d.spp, d.max_depth
+            self.name = d.name.decode()
+        finally:
+            lib.pt_scene_desc_free(C.byref(d))
+
+
+def load_obj(path: str, scale: float = 1.0, translate=(0.0, 0.0, 0.0), mat: int = 0) -> np.ndarray:
+    out = C.c_void_p()
+    n = C.c_int64()
+    t = np.asarray(translate, np.float32)
+    _check(lib.pt_load_obj(path.encode(), scale, _ptr(t), mat, C.byref(out), C.byref(n)), "pt_load_obj")
+    try:
+        buf = (C.c_char * (n.value * OBJECT_DTYPE.itemsize)).from_address(out.value)
+        return np.frombuffer(bytes(buf), dtype=OBJECT_DTYPE).copy()
+    finally:
+        lib.pt_free(out)
+
+
+def morton_keys(objects: np.ndarray, include_origin: bool = True) -> np.ndarray:
+    objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+    keys = np.zeros(len(objects), np.uint64)
+    _check(lib.pt_morton_keys(_ptr(objects) if len(objects) else None, len(objects), int(include_origin),
+                              _ptr(keys) if len(keys) else None), "pt_morton_keys")
+    return keys
+
+
+def quantize_rgba8(rgb: np.ndarray, width: int, height: int) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    out = np.zeros((height, width, 4), np.uint8)
+    _check(lib.pt_quantize_rgba8(_ptr(rgb), width, height, _ptr(out)), "pt_quantize_rgba8")
+    return out
+
+
+def write_png(path: str, rgb: np.ndarray, width: int, height: int) -> None:
+    rgb = np.ascontiguousarray(rgb, np.float32)
+    _check(lib.pt_write_png(path.encode(), _ptr(rgb), width, height), "pt_write_png")
+
+
+class Scene:
+    """Device-resident scene (objects, materials, LBVH) on one GPU."""
+
+    def __init__(self, objects: np.ndarray, materials: np.ndarray, device: int = 0, build: bool = True,
+                 flags: int = PT_BVH_ORIGIN_BOUNDS):
+        self.objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+        self.materials = np.ascontiguousarray(materials, MATERIAL_DTYPE)
+        self.device = device
+        h = C.c_void_p()
+        _check(lib.pt_scene_create(device, _ptr(self.objects) if len(self.objects) else None, len(self.objects),
+                                   _ptr(self.materials) if len(self.materials) else None, len(self.materials),
+                                   C.byref(h)), "pt_scene_create")
+        self.h = h
+        if build:
+            self.build_bvh(flags)
+
+    def build_bvh(self, flags: int = PT_BVH_ORIGIN_BOUNDS) -> None:
+        _check(lib.pt_scene_build_bvh(self.h, flags), "pt_scene_build_bvh")
+
+    def bvh_info(self) -> dict:
+        d, n, b = C.c_int(), C.c_int64(), C.c_int64()
+        _check(lib.pt_scene_bvh_info(self.h, C.byref(d), C.byref(n), C.byref(b)), "pt_scene_bvh_info")
+        return {"depth": d.value, "nodes": n.value, "device_bytes": b.value}
+
+    def download_bvh(self) -> np.ndarray:
+        n = len(self.objects)
+        out = np.zeros(max(0, 2 * n - 1), NODE_DTYPE)
+        _check(lib.pt_scene_download_bvh(self.h, _ptr(out) if len(out) else None), "pt_scene_download_bvh")
+        return out
+
+    def trace(self, rays: np.ndarray, tmin: float = 0.001, tmax: float = float("inf")):
+        rays = np.ascontiguousarray(rays, RAY_DTYPE)
+        hits = np.zeros(len(rays), HIT_DTYPE)
+        st = Stats()
+        _check(lib.pt_trace_closest(self.h, _ptr(rays) if len(rays) else None, len(rays), tmin, tmax,
+                                    _ptr(hits) if len(hits) else None, C.byref(st)), "pt_trace_closest")
+        return hits, st
+
+    def close(self) -> None:
+        if self.h:
+            lib.pt_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Film:
+    """Per-pixel XORWOW streams for the rows of one stripe partition of a frame."""
+
+    def __init__(self, width: int, height: int, seed: int, device: int = 0, stripe_height: int = 8,
+                 n_parts: int = 1, part: int = 0):
+        h = C.c_void_p()
+        _check(lib.pt_film_create(device, width, height, stripe_height, n_parts, part, seed, C.byref(h)),
+               "pt_film_create")
+        self.h = h
+        self.width, self.height = width, height
+        nr, npix = C.c_int(), C.c_int64()
+        _check(lib.pt_film_info(self.h, C.byref(nr), C.byref(npix)), "pt_film_info")
+        self.n_rows, self.n_pixels = nr.value, npix.value
+        self.rows = np.zeros(self.n_rows, np.int32)
+        if self.n_rows:
+            _check(lib.pt_film_rows(self.h, _ptr(self.rows)), "pt_film_rows")
+
+    def get_rng(self) -> np.ndarray:
+        out = np.zeros((self.n_pixels, 6), np.uint32)
+        if self.n_pixels:
+            _check(lib.pt_film_get_rng(self.h, _ptr(out)), "pt_film_get_rng")
+        return out
+
+    def set_rng(self, states: np.ndarray) -> None:
+        states = np.ascontiguousarray(states, np.uint32)
+        assert states.shape == (self.n_pixels, 6)
+        _check(lib.pt_film_set_rng(self.h, _ptr(states)), "pt_film_set_rng")
+
+    def close(self) -> None:
+        if self.h:
+            lib.pt_film_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, out=None, stream=None):
+    """Render spp samples per pixel of the film's rows.  `out` may be a numpy array (host) or
+    an integer device pointer (then `stream` is a hipStream_t handle or None).  Returns
+    (rgb or None, Stats)."""
+    st = Stats()
+    if out is None or isinstance(out, np.ndarray):
+        rgb = out if out is not None else np.zeros((film.n_pixels, 3), np.float32)
+        _check(lib.pt_render(scene.h, film.h, C.byref(camera), spp, max_depth, _ptr(rgb), 0, None, C.byref(st)),
+               "pt_render")
+        return rgb, st
+    _check(lib.pt_render(scene.h, film.h, C.byref(camera), spp, max_depth, C.c_void_p(int(out)), 1,
+                         C.c_void_p(int(stream) if stream else 0), C.byref(st)), "pt_render")
+    return None, st

@@ -1,0 +1,70 @@
+"""Scene / ray generators shared by the CPU and GPU test modules (seeded, deterministic)."""
+import numpy as np
+
+OBJECT_DTYPE = np.dtype([("type", "<i4"), ("mat", "<i4"), ("v", "<f4", (9,))])
+MATERIAL_DTYPE = np.dtype([("type", "<i4"), ("albedo", "<f4", (3,)), ("fuzz", "<f4"), ("ir", "<f4")])
+
+
+def random_soup(n_tri: int, n_sph: int, seed: int, spread: float = 10.0, n_mat: int = 4):
+    """Random triangles and spheres with a mix of all three material types."""
+    rng = np.random.default_rng(seed)
+    objs = np.zeros(n_tri + n_sph, OBJECT_DTYPE)
+    c = rng.uniform(-spread, spread, (n_tri, 3)).astype(np.float32)
+    objs["type"][:n_tri] = 3
+    for k in range(3):
+        objs["v"][:n_tri, 3 * k:3 * k + 3] = c + rng.uniform(-1, 1, (n_tri, 3)).astype(np.float32)
+    objs["type"][n_tri:] = 1
+    objs["v"][n_tri:, :3] = rng.uniform(-spread, spread, (n_sph, 3)).astype(np.float32)
+    objs["v"][n_tri:, 3] = rng.uniform(0.2, 1.5, n_sph).astype(np.float32)
+    objs["mat"] = rng.integers(0, n_mat, len(objs))
+    perm = rng.permutation(len(objs))
+    objs = objs[perm]
+    mats = np.zeros(n_mat, MATERIAL_DTYPE)
+    for m in range(n_mat):
+        t = [1, 2, 4, 1][m % 4]
+        mats[m]["type"] = t
+        mats[m]["albedo"] = rng.uniform(0.2, 0.9, 3)
+        mats[m]["fuzz"] = 0.3 if t == 2 else 0.0
+        mats[m]["ir"] = 1.5 if t == 4 else 0.0
+    return objs, mats
+
+
+def duplicate_centroids(n: int):
+    """n identical tiny triangles (all Morton codes equal: exercises objID tie-breaking)."""
+    objs = np.zeros(n, OBJECT_DTYPE)
+    objs["type"] = 3
+    objs["v"][:] = [0, 0, 0, 1, 0, 0, 0, 1, 0]
+    objs["mat"] = 0
+    mats = np.zeros(1, MATERIAL_DTYPE)
+    mats["type"] = 1
+    mats["albedo"] = 0.5
+    return objs, mats
+
+
+def random_rays(n: int, seed: int, center=(0, 0, 0), radius: float = 15.0, objects=None):
+    """Rays from a sphere of origins toward the scene, plus rays aimed at object centres."""
+    rng = np.random.default_rng(seed)
+    o = rng.normal(size=(n, 3))
+    o = o / np.linalg.norm(o, axis=1, keepdims=True) * radius + np.asarray(center)
+    tgt = rng.uniform(-radius / 2, radius / 2, (n, 3)) + np.asarray(center)
+    if objects is not None and len(objects):
+        k = rng.integers(0, len(objects), n // 2)
+        v = objects["v"][k]
+        cen = np.where((objects["type"][k] == 1)[:, None], v[:, :3], (v[:, 0:3] + v[:, 3:6] + v[:, 6:9]) / 3)
+        tgt[: n // 2] = cen
+    d = tgt - o
+    rays = np.zeros((n, 6), np.float32)
+    rays[:, :3] = o
+    rays[:, 3:] = d * rng.uniform(0.3, 3.0, (n, 1))   # unnormalised, as the reference's rays
+    # a few axis-aligned directions (zero components -> infinite slab reciprocals)
+    m = min(64, n)
+    rays[:m, 3:] = 0
+    rays[:m, 3 + (np.arange(m) % 3)] = np.where(np.arange(m) % 2, 1.0, -1.0)
+    return rays
+
+
+def rays_to_struct(rays: np.ndarray, ray_dtype) -> np.ndarray:
+    out = np.zeros(len(rays), ray_dtype)
+    out["o"] = rays[:, :3]
+    out["d"] = rays[:, 3:]
+    return out

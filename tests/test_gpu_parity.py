@@ -1,0 +1,261 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU restatement (oracle/).
+
+The kernels evaluate every expression in the reference's operation order with contraction
+off, so the bar is BIT-EXACT for everything: LBVH topology and boxes, closest-hit records,
+per-pixel RNG streams and rendered images (fp32 tolerance 0 ulp).  Full-size configurations
+are covered through size-independent properties (determinism, stripe invariance, subsets of
+rows checked against the oracle).
+"""
+import numpy as np
+import pytest
+
+from helpers import duplicate_centroids, random_rays, random_soup, rays_to_struct
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def assert_nodes_equal(g, o):
+    for f in ("left", "right", "parent", "objid"):
+        np.testing.assert_array_equal(g[f], o[f], err_msg=f)
+    np.testing.assert_array_equal(bits(g["bmin"]), bits(o["bmin"]))
+    np.testing.assert_array_equal(bits(g["bmax"]), bits(o["bmax"]))
+
+
+def assert_hits_equal(g, o):
+    for f in ("hit", "obj", "mat", "front_face"):
+        np.testing.assert_array_equal(g[f], o[f], err_msg=f)
+    h = g["hit"] == 1
+    for f in ("t", "p", "n"):
+        np.testing.assert_array_equal(bits(g[f][h]), bits(o[f][h]), err_msg=f)
+
+
+SCENES = ["triangle_world", "random_world", "test_world", "rtiow", "cornell", "bunny_cornell"]
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_lbvh_matches_oracle(pt, orc, gpu, name):
+    p = pt.Preset(name)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    nodes = s.download_bvh()
+    ref = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    assert_nodes_equal(nodes, ref)
+    assert s.bvh_info()["depth"] == orc.bvh_depth(ref, len(p.objects))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 64, 1000])
+def test_lbvh_small_and_duplicates(pt, orc, gpu, n):
+    for objs, mats in (random_soup(n - n // 2, n // 2, seed=n), duplicate_centroids(n)):
+        s = pt.Scene(objs, mats, device=gpu)
+        assert_nodes_equal(s.download_bvh(), orc.build_lbvh(objs, orc.morton_keys(objs), tight=True))
+
+
+def test_lbvh_large_soup(pt, orc, gpu):
+    objs, mats = random_soup(150_000, 50_000, seed=7, spread=100.0)
+    s = pt.Scene(objs, mats, device=gpu)
+    assert_nodes_equal(s.download_bvh(), orc.build_lbvh(objs, orc.morton_keys(objs), tight=True))
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_trace_closest_matches_oracle(pt, orc, gpu, name):
+    p = pt.Preset(name)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    ref_nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    lo = p.objects["v"][:, :3].min(0)
+    hi = p.objects["v"][:, :3].max(0)
+    center = np.clip((lo + hi) / 2, -1e3, 1e3)
+    radius = float(min(np.linalg.norm(hi - lo), 3000.0)) * 0.75 + 1.0
+    rays = random_rays(4096, seed=1, center=center, radius=radius, objects=p.objects)
+    hits, st = s.trace(rays_to_struct(rays, pt.RAY_DTYPE))
+    ref, rst = orc.trace(p.objects, ref_nodes, rays)
+    assert_hits_equal(hits, ref)
+    assert hits["hit"].sum() > 100
+    assert st.node_visits == rst.node_visits and st.tri_tests == rst.tri_tests
+    assert st.sphere_tests == rst.sphere_tests
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_trace_random_soup(pt, orc, gpu, seed):
+    objs, mats = random_soup(3000, 500, seed=seed)
+    s = pt.Scene(objs, mats, device=gpu)
+    rays = random_rays(8192, seed=seed + 10, objects=objs)
+    hits, _ = s.trace(rays_to_struct(rays, pt.RAY_DTYPE))
+    ref, _ = orc.trace(objs, orc.build_lbvh(objs, orc.morton_keys(objs), tight=True), rays)
+    assert_hits_equal(hits, ref)
+    brute, _ = orc.trace(objs, None, rays, brute=True)   # BVH closest hit == brute force
+    np.testing.assert_array_equal(ref["obj"], brute["obj"])
+
+
+def test_trace_tmin_tmax_window(pt, orc, gpu):
+    objs, mats = random_soup(500, 100, seed=3)
+    s = pt.Scene(objs, mats, device=gpu)
+    rays = random_rays(2048, seed=4, objects=objs)
+    for tmin, tmax in ((0.001, 5.0), (2.0, 40.0), (0.0, np.inf)):
+        hits, _ = s.trace(rays_to_struct(rays, pt.RAY_DTYPE), tmin, tmax)
+        ref, _ = orc.trace(objs, orc.build_lbvh(objs, orc.morton_keys(objs), tight=True), rays, tmin, tmax)
+        assert_hits_equal(hits, ref)
+
+
+@pytest.mark.parametrize("parts", [1, 3])
+def test_rng_streams_match_curand_init(pt, orc, gpu, parts):
+    w, h = 97, 23
+    for part in range(parts):
+        f = pt.Film(w, h, seed=12345, device=gpu, stripe_height=4, n_parts=parts, part=part)
+        np.testing.assert_array_equal(f.get_rng(), orc.film_states(12345, w, f.rows))
+
+
+def test_rng_streams_far_pixels(pt, orc, gpu):
+    """Pixel indices up to 1920*1080 exercise 21 jump matrices."""
+    w, h = 1920, 1080
+    f = pt.Film(w, h, seed=987654321987, device=gpu, stripe_height=8, n_parts=135, part=134)
+    np.testing.assert_array_equal(f.get_rng(), orc.film_states(987654321987, w, f.rows))
+
+
+def render_both(pt, orc, gpu, p, w, h, spp, depth, seed=1, parts=1, part=0, stripe=8):
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, seed, device=gpu, stripe_height=stripe, n_parts=parts, part=part)
+    rgb, st = pt.render(s, f, p.camera, spp, depth)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    states = orc.film_states(seed, w, f.rows)
+    ref, rst = orc.render(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, f.rows, spp, depth,
+                          states, nthreads=8)
+    return rgb, st, f.get_rng(), ref, rst, states, f
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth", [
+    ("rtiow", 64, 36, 4, 50),            # C1 scene: dielectric + metal + lambert spheres
+    ("triangle_world", 80, 45, 4, 50),   # reference default scene
+    ("random_world", 64, 36, 2, 50),
+    ("test_world", 48, 27, 4, 50),
+    ("cornell", 64, 64, 8, 8),           # C2 scene
+    ("bunny_cornell", 96, 54, 2, 50),    # C3 scene
+])
+def test_render_bit_exact(pt, orc, gpu, name, w, h, spp, depth):
+    p = pt.Preset(name, w, h)
+    rgb, st, rng_after, ref, rst, ref_states, _ = render_both(pt, orc, gpu, p, w, h, spp, depth)
+    np.testing.assert_array_equal(bits(rgb), bits(ref))
+    np.testing.assert_array_equal(rng_after, ref_states)   # streams advanced identically
+    assert st.rays == rst.rays and st.paths == rst.paths == w * h * spp
+    assert st.node_visits == rst.node_visits
+
+
+@pytest.mark.parametrize("w,h,stripe", [(37, 19, 3), (50, 30, 8), (8, 8, 1)])
+def test_render_stripes_assemble_to_full_frame(pt, orc, gpu, w, h, stripe):
+    p = pt.Preset("rtiow", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    full, _ = pt.render(s, pt.Film(w, h, 5, device=gpu), p.camera, 3, 50)
+    full = full.reshape(h, w, 3)
+    for parts in (2, 3):
+        img = np.zeros_like(full)
+        for part in range(parts):
+            f = pt.Film(w, h, 5, device=gpu, stripe_height=stripe, n_parts=parts, part=part)
+            rgb, _ = pt.render(s, f, p.camera, 3, 50)
+            img[f.rows] = rgb.reshape(f.n_rows, w, 3)
+        np.testing.assert_array_equal(bits(img), bits(full))
+
+
+def test_render_edge_cases(pt, orc, gpu):
+    p = pt.Preset("rtiow", 16, 9)
+    for depth in (0, 1):
+        rgb, st, _, ref, _, _, _ = render_both(pt, orc, gpu, p, 16, 9, 2, depth)
+        np.testing.assert_array_equal(bits(rgb), bits(ref))
+        if depth == 0:
+            assert st.rays == 0
+    # single object (root is a leaf) and an empty-ish scene
+    objs, mats = random_soup(0, 1, seed=1)
+    objs["v"][0, :3] = [0, 0, -1]
+    objs["v"][0, 3] = 0.5
+    one = pt.Preset("rtiow", 16, 9)
+    one.objects, one.materials = objs, mats
+    rgb, _, _, ref, _, _, _ = render_both(pt, orc, gpu, one, 16, 9, 2, 5)
+    np.testing.assert_array_equal(bits(rgb), bits(ref))
+
+
+def test_render_continues_streams(pt, orc, gpu):
+    """Two calls of spp=2 continue the per-pixel streams exactly like the reference's devStates."""
+    w, h = 24, 16
+    p = pt.Preset("cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, 9, device=gpu)
+    a, _ = pt.render(s, f, p.camera, 2, 8)
+    b, _ = pt.render(s, f, p.camera, 2, 8)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    states = orc.film_states(9, w, f.rows)
+    cam = pt.camera_to_array(p.camera)
+    ra, _ = orc.render(p.objects, p.materials, nodes, cam, w, h, f.rows, 2, 8, states, 4)
+    rb, _ = orc.render(p.objects, p.materials, nodes, cam, w, h, f.rows, 2, 8, states, 4)
+    np.testing.assert_array_equal(bits(a), bits(ra))
+    np.testing.assert_array_equal(bits(b), bits(rb))
+    assert not np.array_equal(a, b)
+
+
+def test_full_size_c3_properties(pt, orc, gpu):
+    """C3 frame size (1920x1080) at 1 spp: deterministic, finite, stripe-invariant, and a
+    subset of rows bit-exact against the oracle."""
+    p = pt.Preset("bunny_cornell")
+    w, h = p.width, p.height
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    a, st = pt.render(s, pt.Film(w, h, 1, device=gpu), p.camera, 1, p.max_depth)
+    b, _ = pt.render(s, pt.Film(w, h, 1, device=gpu), p.camera, 1, p.max_depth)
+    np.testing.assert_array_equal(bits(a), bits(b))
+    assert np.isfinite(a).all() and (a >= 0).all()
+    assert st.paths == w * h and st.rays >= st.paths
+    # rows 0, 540, 1079 through the oracle
+    img = a.reshape(h, w, 3)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    rows = np.array([0, 540, 1079], np.int32)
+    states = orc.film_states(1, w, rows)
+    ref, _ = orc.render(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, rows, 1, p.max_depth,
+                        states, 8)
+    np.testing.assert_array_equal(bits(img[rows].reshape(-1, 3)), bits(ref))
+    # 8-way stripes reproduce the full frame (the multi-GPU layout)
+    img8 = np.zeros_like(img)
+    for part in range(8):
+        f = pt.Film(w, h, 1, device=gpu, stripe_height=8, n_parts=8, part=part)
+        rgb, _ = pt.render(s, f, p.camera, 1, p.max_depth)
+        img8[f.rows] = rgb.reshape(f.n_rows, w, 3)
+    np.testing.assert_array_equal(bits(img8), bits(img))
+
+
+def test_full_size_c5_bvh_and_trace(pt, orc, gpu):
+    """C5 (1,043,312 triangles): GPU LBVH equals the oracle's, and closest hits agree."""
+    p = pt.Preset("bunny_field")
+    assert len(p.objects) == 1_043_312
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    nodes = s.download_bvh()
+    ref = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    assert_nodes_equal(nodes, ref)
+    rays = random_rays(4096, seed=5, center=(278, 150, 280), radius=700, objects=p.objects)
+    hits, _ = s.trace(rays_to_struct(rays, pt.RAY_DTYPE))
+    rh, _ = orc.trace(p.objects, ref, rays)
+    assert_hits_equal(hits, rh)
+
+
+def test_device_output_pointer(gpu):
+    """pt_render into a caller-owned device buffer (a torch tensor) on the caller's stream.
+    Runs in a child process that imports torch BEFORE libpt.so, as bench.py does, so that both
+    share one HIP runtime."""
+    import subprocess
+    import sys
+    code = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+import ptamd as pt
+p = pt.Preset("cornell", 32, 32)
+s = pt.Scene(p.objects, p.materials, device=0)
+host, _ = pt.render(s, pt.Film(32, 32, 3, device=0), p.camera, 2, 8)
+out = torch.zeros((32 * 32, 3), dtype=torch.float32, device="cuda:0")
+stream = torch.cuda.current_stream()
+_, st = pt.render(s, pt.Film(32, 32, 3, device=0), p.camera, 2, 8, out=out.data_ptr(), stream=stream.cuda_stream)
+torch.cuda.synchronize()
+assert np.array_equal(out.cpu().numpy().view(np.uint32), host.view(np.uint32))
+print("ok", st.rays)
+"""
+    import os
+    pydir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "path-tracer-cuda-opengl_amd",
+                         "python")
+    r = subprocess.run([sys.executable, "-c", code, pydir], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
