@@ -27,6 +27,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"))
 import ptamd  # noqa: E402
+import ptdist  # noqa: E402
 
 METRIC = "Mray/s + ms/frame, bunny-in-Cornell 1920×1080 @1024spp, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -91,8 +92,7 @@ def main() -> None:
     w, h, depth = preset.width, preset.height, preset.max_depth
     scene = ptamd.Scene(preset.objects, preset.materials, device=local)
     film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
-    stripes = (h + STRIPE - 1) // STRIPE
-    max_rows = ((stripes + world - 1) // world) * STRIPE
+    max_rows = ptdist.max_rows(h, STRIPE, world)
     local_buf = torch.zeros((max_rows * w * 3,), dtype=torch.float32, device=dev)
     gathered = torch.empty((world * max_rows * w * 3,), dtype=torch.float32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
@@ -133,12 +133,8 @@ def main() -> None:
         total_rays = float(rays)
 
     if rank == 0:
-        if world > 1:   # un-permute the stripes (proves the gathered frame is complete)
-            img = torch.empty((h, w, 3), dtype=torch.float32, device=dev)
-            g = gathered.view(world, max_rows, w, 3)
-            for r in range(world):
-                rows = torch.tensor([rr for rr in range(h) if (rr // STRIPE) % world == r], device=dev)
-                img[rows] = g[r, : len(rows)]
+        if world > 1:   # un-permute the stripes of the last frame (rank 0 holds the full image)
+            ptdist.assemble(gathered, h, w, STRIPE, world)
             torch.cuda.synchronize(dev)
         achieved = (kbytes / 1e9) / (kms / 1e3) if kms > 0 else 0.0
         out = {

@@ -1,0 +1,43 @@
+"""Row-stripe partition of a frame across ranks and the gather that reassembles it.
+
+Stripe s (rows [s*stripe, (s+1)*stripe)) belongs to rank s % world, which interleaves cheap
+(sky) and expensive (geometry) rows across GPUs.  Every rank renders its rows packed in
+order into a buffer padded to `max_rows(...)` rows, one all-gather (RCCL over xGMI on the GPU
+box, gloo in the CPU tests) concatenates the buffers, and `assemble` un-permutes them.
+The RNG is keyed by the GLOBAL pixel index (curand_init(seed, pixel, 0), main.cu:268), so
+the assembled frame is bit-identical to a single-GPU render.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def stripe_rows(height: int, stripe: int, world: int, rank: int) -> np.ndarray:
+    r = np.arange(height)
+    return r[(r // stripe) % world == rank].astype(np.int32)
+
+
+def max_rows(height: int, stripe: int, world: int) -> int:
+    stripes = (height + stripe - 1) // stripe
+    return ((stripes + world - 1) // world) * stripe
+
+
+def assemble(gathered, height: int, width: int, stripe: int, world: int):
+    """gathered: array/tensor of shape (world, max_rows, width, 3) -> (height, width, 3)."""
+    mr = max_rows(height, stripe, world)
+    g = gathered.reshape(world, mr, width, 3)
+    try:  # torch tensor
+        import torch
+        if isinstance(g, torch.Tensor):
+            img = torch.empty((height, width, 3), dtype=g.dtype, device=g.device)
+            for r in range(world):
+                rows = torch.as_tensor(stripe_rows(height, stripe, world, r), device=g.device, dtype=torch.long)
+                img[rows] = g[r, : len(rows)]
+            return img
+    except ImportError:
+        pass
+    img = np.empty((height, width, 3), dtype=g.dtype)
+    for r in range(world):
+        rows = stripe_rows(height, stripe, world, r)
+        img[rows] = g[r, : len(rows)]
+    return img
