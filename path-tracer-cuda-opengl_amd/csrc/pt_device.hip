@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -311,6 +312,7 @@ struct RenderParams {
     int tiles_x, ntiles;
     int spp, max_depth;
     float invW, invH, invSpp;
+    int leafBatch, shadeBatch;                // wavefront scheduler thresholds (lanes)
 };
 
 __device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
@@ -396,6 +398,204 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
                 }
             }
         }
+        float* outp = P.out + 3 * idx;   // main.cu:290-293
+        outp[0] = sqrtf(sum.x * P.invSpp);
+        outp[1] = sqrtf(sum.y * P.invSpp);
+        outp[2] = sqrtf(sum.z * P.invSpp);
+        P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+    }
+    waveReduceAdd(P.counters + 0, c.rays);
+    waveReduceAdd(P.counters + 1, c.visits);
+    waveReduceAdd(P.counters + 2, c.tris);
+    waveReduceAdd(P.counters + 3, c.spheres);
+    waveReduceAdd(P.counters + 4, paths);
+}
+
+
+// Wavefront-scheduled render kernel.  Each lane runs the same per-pixel program as
+// renderKernel (identical operation order => identical results), decomposed into steps:
+//   NODE : pop/visit one BVH node: test the left child box (a hit leaf => LEAF first), then
+//          the right child box, push hit internal children, pop the next node
+//   LEAF : one primitive test (cuda_object.h:44-92), then resume the node's right child
+//   SHADE: hit record + scatter + path bookkeeping + next camera ray (main.cu:26-36, 283-289)
+// Every loop iteration runs ONE step kind for the lanes in that phase; the kind is chosen from
+// wave-wide __ballot counts (uniform scalar branch), so a lane never waits for other lanes'
+// primitive tests or shading inside a node step.  Lanes waiting for their phase idle briefly.
+enum : int { PH_NODE = 0, PH_LEAF = 1, PH_SHADE = 2, PH_DONE = 3 };
+
+template <int STACK>
+__global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    const int tile = xcdTile(blockIdx.x, P.ntiles);
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int col = tx * 8 + (lane & 7);
+    const int lrow = ty * 8 + (lane >> 3);
+    const bool valid = col < P.width && lrow < P.nrows;
+    const size_t idx = valid ? (size_t)lrow * P.width + col : 0;
+    const float fcol = (float)col;
+    const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
+    const DevScene& S = P.S;
+    uint32_t* my = stk + lane;
+    Counters c{0, 0, 0, 0};
+    uint32_t paths = 0;
+
+    Xorwow g{0, 0, 0, 0, 0, 0};
+    if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+    float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
+    float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
+    float closest = 0.0f;
+    int best = -1, depthLeft = 0, sample = 0, node = 0, sp = 0;
+    uint32_t leafRef = 0;
+    bool skipLeft = false, resumeNode = false;
+    int phase = PH_DONE;
+
+    // Start the traversal of the current ray (o, d).
+    auto beginRay = [&]() {
+        c.rays++;
+        depthLeft--;
+        closest = __builtin_inff();
+        best = -1;
+        sp = 0;
+        node = 0;
+        skipLeft = false;
+        if (S.nprims <= 0) {
+            phase = PH_SHADE;
+        } else if (S.nprims == 1) {   // root is a leaf (render_manager.h:92-98)
+            leafRef = kLeafBit | (__float_as_uint(S.prims[2].w) ? kSphereBit : 0u);
+            resumeNode = false;
+            phase = PH_LEAF;
+        } else {
+            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+            phase = PH_NODE;
+        }
+    };
+    // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
+    auto newPath = [&]() {
+        float u = (fcol + g.uniform()) * P.invW;
+        float v = (frow + g.uniform()) * P.invH;
+        o = P.cam.pos;
+        d = sub(add(add(P.cam.ll, scale(u, P.cam.hor)), scale(v, P.cam.ver)), P.cam.pos);
+        att = f3(1.0f, 1.0f, 1.0f);
+        depthLeft = P.max_depth;
+        paths++;
+    };
+    auto popOrShade = [&]() {
+        if (sp == 0) {
+            phase = PH_SHADE;
+        } else {
+            sp--;
+            node = (int)my[sp * kWave];
+            skipLeft = false;
+            phase = PH_NODE;
+        }
+    };
+
+    if (valid) {
+        if (P.max_depth <= 0) {
+            for (; sample < P.spp; sample++) { newPath(); sum = add(sum, sky(d, att)); }
+        } else if (P.spp > 0) {
+            newPath();
+            beginRay();
+        }
+    }
+
+    for (;;) {
+        const uint64_t mN = __ballot(phase == PH_NODE);
+        const uint64_t mL = __ballot(phase == PH_LEAF);
+        const uint64_t mS = __ballot(phase == PH_SHADE);
+        if ((mN | mL | mS) == 0) break;
+        const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
+        if (nS > 0 && (nS >= P.shadeBatch || nN + nL == 0)) {
+            // ---------------------------------------------------------------- SHADE
+            if (phase == PH_SHADE) {
+                bool done = false;
+                float3 contrib = f3(0.0f, 0.0f, 0.0f);
+                if (best < 0) {
+                    contrib = sky(d, att);
+                    done = true;
+                } else {
+                    HitRec h = makeHit(S, best, closest, o, d);
+                    float3 na;
+                    if (!scatter(S, h, d, na, g)) {
+                        done = true;
+                    } else {
+                        att = mul(att, na);
+                        o = h.p;
+                        if (depthLeft == 0) { contrib = sky(d, att); done = true; }
+                    }
+                }
+                if (done) {
+                    sum = add(sum, contrib);
+                    if (++sample == P.spp) {
+                        phase = PH_DONE;
+                    } else {
+                        newPath();
+                        beginRay();
+                    }
+                } else {
+                    beginRay();
+                }
+            }
+        } else if (nL > 0 && (nL >= P.leafBatch || nN == 0)) {
+            // ---------------------------------------------------------------- LEAF
+            if (phase == PH_LEAF) {
+                primTest(S, leafRef, o, d, 0.001f, closest, best, c);
+                if (resumeNode) {
+                    skipLeft = true;
+                    phase = PH_NODE;
+                } else {
+                    popOrShade();
+                }
+            }
+        } else {
+            // ---------------------------------------------------------------- NODE
+            if (phase == PH_NODE) {
+                const float4* np = S.nodes + 4 * (size_t)node;
+                const float4 a = np[0], b = np[1], q = np[2], r = np[3];
+                const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
+                bool toLeaf = false, overflow = false;
+                if (!skipLeft) {
+                    c.visits++;
+                    if (slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest)) {
+                        if (lref & kLeafBit) {
+                            leafRef = lref;
+                            resumeNode = true;
+                            toLeaf = true;
+                        } else if (sp < STACK) {
+                            my[sp * kWave] = lref;
+                            sp++;
+                        } else {
+                            overflow = true;
+                        }
+                    }
+                }
+                if (!toLeaf && !overflow) {
+                    if (slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest)) {
+                        if (rref & kLeafBit) {
+                            leafRef = rref;
+                            resumeNode = false;
+                            toLeaf = true;
+                        } else if (sp < STACK) {
+                            my[sp * kWave] = rref;
+                            sp++;
+                        } else {
+                            overflow = true;
+                        }
+                    }
+                }
+                if (overflow) {
+                    atomicOr(S.err, 2u);
+                    phase = PH_SHADE;
+                } else if (toLeaf) {
+                    phase = PH_LEAF;
+                } else {
+                    popOrShade();
+                }
+            }
+        }
+    }
+    if (valid) {
         float* outp = P.out + 3 * idx;   // main.cu:290-293
         outp[0] = sqrtf(sum.x * P.invSpp);
         outp[1] = sqrtf(sum.y * P.invSpp);
@@ -624,6 +824,13 @@ int devAlloc(DevBuf& b, size_t bytes) {
     return PT_OK;
 }
 
+int envInt(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    int x = std::atoi(v);
+    return x < 1 ? 1 : (x > 64 ? 64 : x);
+}
+
 int stackFor(int depth) {
     const int need = depth + 1;
     for (int s : {16, 32, 48, 64, 80})
@@ -667,7 +874,8 @@ int setDevice(int dev) {
 
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
-    renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
+    if (P.leafBatch > 0) renderKernelWF<S><<<P.ntiles, kWave, 0, st>>>(P);
+    else renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
 }
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
     switch (stack) {
@@ -1074,6 +1282,13 @@ int pt_render(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_de
     P.invW = 1.0f / (float)f->width;    // main.cu:281
     P.invH = 1.0f / (float)f->height;
     P.invSpp = 1.0f / (float)spp;
+    // Scheduler: PT_RENDER_KERNEL=simple selects the ray-synchronous kernel; PT_LEAF_BATCH /
+    // PT_SHADE_BATCH tune the wavefront kernel's step thresholds (lanes out of 64).
+    P.leafBatch = envInt("PT_LEAF_BATCH", 16);
+    P.shadeBatch = envInt("PT_SHADE_BATCH", 24);
+    if (const char* k = std::getenv("PT_RENDER_KERNEL")) {
+        if (std::string(k) == "simple") P.leafBatch = 0;
+    }
     const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));

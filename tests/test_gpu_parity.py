@@ -125,6 +125,19 @@ def render_both(pt, orc, gpu, p, w, h, spp, depth, seed=1, parts=1, part=0, stri
     return rgb, st, f.get_rng(), ref, rst, states, f
 
 
+KERNELS = [("wavefront", "16", "24"), ("simple", "16", "24"), ("wavefront", "1", "1"), ("wavefront", "64", "64"),
+           ("wavefront", "5", "50")]
+
+
+@pytest.fixture(params=KERNELS, ids=lambda k: f"{k[0]}-L{k[1]}-S{k[2]}")
+def kernel(request, monkeypatch):
+    name, leaf, shade = request.param
+    monkeypatch.setenv("PT_RENDER_KERNEL", name)
+    monkeypatch.setenv("PT_LEAF_BATCH", leaf)
+    monkeypatch.setenv("PT_SHADE_BATCH", shade)
+    return request.param
+
+
 @pytest.mark.parametrize("name,w,h,spp,depth", [
     ("rtiow", 64, 36, 4, 50),            # C1 scene: dielectric + metal + lambert spheres
     ("triangle_world", 80, 45, 4, 50),   # reference default scene
@@ -133,7 +146,7 @@ def render_both(pt, orc, gpu, p, w, h, spp, depth, seed=1, parts=1, part=0, stri
     ("cornell", 64, 64, 8, 8),           # C2 scene
     ("bunny_cornell", 96, 54, 2, 50),    # C3 scene
 ])
-def test_render_bit_exact(pt, orc, gpu, name, w, h, spp, depth):
+def test_render_bit_exact(pt, orc, gpu, kernel, name, w, h, spp, depth):
     p = pt.Preset(name, w, h)
     rgb, st, rng_after, ref, rst, ref_states, _ = render_both(pt, orc, gpu, p, w, h, spp, depth)
     np.testing.assert_array_equal(bits(rgb), bits(ref))
@@ -143,7 +156,7 @@ def test_render_bit_exact(pt, orc, gpu, name, w, h, spp, depth):
 
 
 @pytest.mark.parametrize("w,h,stripe", [(37, 19, 3), (50, 30, 8), (8, 8, 1)])
-def test_render_stripes_assemble_to_full_frame(pt, orc, gpu, w, h, stripe):
+def test_render_stripes_assemble_to_full_frame(pt, orc, gpu, kernel, w, h, stripe):
     p = pt.Preset("rtiow", w, h)
     s = pt.Scene(p.objects, p.materials, device=gpu)
     full, _ = pt.render(s, pt.Film(w, h, 5, device=gpu), p.camera, 3, 50)
@@ -157,7 +170,7 @@ def test_render_stripes_assemble_to_full_frame(pt, orc, gpu, w, h, stripe):
         np.testing.assert_array_equal(bits(img), bits(full))
 
 
-def test_render_edge_cases(pt, orc, gpu):
+def test_render_edge_cases(pt, orc, gpu, kernel):
     p = pt.Preset("rtiow", 16, 9)
     for depth in (0, 1):
         rgb, st, _, ref, _, _, _ = render_both(pt, orc, gpu, p, 16, 9, 2, depth)
