@@ -412,16 +412,30 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 }
 
 
-// Wavefront-scheduled render kernel.  Each lane runs the same per-pixel program as
-// renderKernel (identical operation order => identical results), decomposed into steps:
-//   NODE : pop/visit one BVH node: test the left child box (a hit leaf => LEAF first), then
-//          the right child box, push hit internal children, pop the next node
-//   LEAF : one primitive test (cuda_object.h:44-92), then resume the node's right child
-//   SHADE: hit record + scatter + path bookkeeping + next camera ray (main.cu:26-36, 283-289)
-// Every loop iteration runs ONE step kind for the lanes in that phase; the kind is chosen from
-// wave-wide __ballot counts (uniform scalar branch), so a lane never waits for other lanes'
-// primitive tests or shading inside a node step.  Lanes waiting for their phase idle briefly.
-enum : int { PH_NODE = 0, PH_LEAF = 1, PH_SHADE = 2, PH_DONE = 3 };
+// Wavefront-scheduled render kernel (speculative while-while, exact).
+// Each lane runs the same per-pixel program as renderKernel, decomposed into three step kinds;
+// every loop iteration runs ONE kind, chosen from wave-wide __ballot counts (a uniform scalar
+// branch), for all lanes that have that kind of work:
+//   NODE : visit one internal node: test both child boxes against the lane's current `closest`;
+//          hit leaves are appended to the lane's leaf queue (DFS order), hit internal children
+//          are pushed / descended into (the reference's order: right subtree first).
+//   LEAF : take the oldest queued leaf, RE-TEST its box against the current `closest`, then run
+//          the primitive test (cuda_object.h:44-92).
+//   SHADE: hit record + scatter + path bookkeeping + next ray (main.cu:26-36, 283-289).
+// Exactness: leaves are tested in the reference's DFS order, each with the same `closest` the
+// reference would use (only primitive tests change `closest`), and a box that fails with a
+// stale (larger) `closest` also fails with the true one (the slab interval shrinks
+// monotonically with tmax and with the box).  Node boxes tested with a stale `closest` only
+// add visits.  So the sequence of primitive tests -- and every pixel -- is identical to the
+// reference order; node visit counts may be higher.  Lanes keep traversing while leaves wait,
+// so primitive tests run with many lanes active instead of one or two.
+constexpr int kLeafQ = 4;
+
+__device__ __forceinline__ bool slabRec(const float4& a, const float4& b, const float4& q, int side, float3 o,
+                                        float3 inv, float tmin, float tmax) {
+    return side == 0 ? slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, tmax)
+                     : slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, tmin, tmax);
+}
 
 template <int STACK>
 __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
@@ -445,33 +459,29 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
     float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
-    int best = -1, depthLeft = 0, sample = 0, node = 0, sp = 0;
-    uint32_t leafRef = 0;
-    bool skipLeft = false, resumeNode = false;
-    int phase = PH_DONE;
+    int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: (parent node << 1) | side
+    bool active = false;
 
-    // Start the traversal of the current ray (o, d).
-    auto beginRay = [&]() {
+    auto beginRay = [&]() {   // start the closest-hit query of (o, d)
         c.rays++;
         depthLeft--;
         closest = __builtin_inff();
         best = -1;
         sp = 0;
-        node = 0;
-        skipLeft = false;
-        if (S.nprims <= 0) {
-            phase = PH_SHADE;
-        } else if (S.nprims == 1) {   // root is a leaf (render_manager.h:92-98)
-            leafRef = kLeafBit | (__float_as_uint(S.prims[2].w) ? kSphereBit : 0u);
-            resumeNode = false;
-            phase = PH_LEAF;
+        qn = 0;
+        if (S.nprims <= 1) {
+            node = -1;
+            if (S.nprims == 1) {   // root is a leaf: tested without a box test (render_manager.h:92-98)
+                const uint32_t ref = kLeafBit | (__float_as_uint(S.prims[2].w) ? kSphereBit : 0u);
+                primTest(S, ref, o, d, 0.001f, closest, best, c);
+            }
         } else {
             inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-            phase = PH_NODE;
+            node = 0;
         }
     };
-    // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
-    auto newPath = [&]() {
+    auto newPath = [&]() {   // main.cu:284-286 + camera::get_ray (lens/time draws skipped)
         float u = (fcol + g.uniform()) * P.invW;
         float v = (frow + g.uniform()) * P.invH;
         o = P.cam.pos;
@@ -480,16 +490,6 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
         depthLeft = P.max_depth;
         paths++;
     };
-    auto popOrShade = [&]() {
-        if (sp == 0) {
-            phase = PH_SHADE;
-        } else {
-            sp--;
-            node = (int)my[sp * kWave];
-            skipLeft = false;
-            phase = PH_NODE;
-        }
-    };
 
     if (valid) {
         if (P.max_depth <= 0) {
@@ -497,18 +497,75 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
         } else if (P.spp > 0) {
             newPath();
             beginRay();
+            active = true;
         }
     }
 
     for (;;) {
-        const uint64_t mN = __ballot(phase == PH_NODE);
-        const uint64_t mL = __ballot(phase == PH_LEAF);
-        const uint64_t mS = __ballot(phase == PH_SHADE);
+        const bool wantNode = node >= 0 && qn <= kLeafQ - 2;
+        const bool wantLeaf = qn > 0;
+        const bool wantShade = active && node < 0 && qn == 0;
+        const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
-        if (nS > 0 && (nS >= P.shadeBatch || nN + nL == 0)) {
-            // ---------------------------------------------------------------- SHADE
-            if (phase == PH_SHADE) {
+        int kind;   // 0 node, 1 leaf, 2 shade
+        if (nN == 0) kind = nL > 0 ? 1 : 2;
+        else if (nL >= P.leafBatch) kind = 1;
+        else if (nS >= P.shadeBatch) kind = 2;
+        else kind = 0;
+
+        if (kind == 0) {
+            // ------------------------------------------------------------------ NODE
+            if (wantNode) {
+                c.visits++;
+                const float4* np = S.nodes + 4 * (size_t)node;
+                const float4 a = np[0], b = np[1], q = np[2], r = np[3];
+                const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
+                const bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest);
+                const bool hr = slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest);
+                const uint32_t e0 = (uint32_t)node << 1;
+                // append hit leaves in order (left, then right)
+                if (hl && (lref & kLeafBit)) {
+                    q0 = qn == 0 ? e0 : q0; q1 = qn == 1 ? e0 : q1; q2 = qn == 2 ? e0 : q2; q3 = qn == 3 ? e0 : q3;
+                    qn++;
+                }
+                if (hr && (rref & kLeafBit)) {
+                    const uint32_t e1 = e0 | 1u;
+                    q0 = qn == 0 ? e1 : q0; q1 = qn == 1 ? e1 : q1; q2 = qn == 2 ? e1 : q2; q3 = qn == 3 ? e1 : q3;
+                    qn++;
+                }
+                const bool il = hl && !(lref & kLeafBit), ir = hr && !(rref & kLeafBit);
+                // push left then right, pop: descend straight into the child that would be popped
+                if (ir) {
+                    if (il) {
+                        if (sp < STACK) { my[sp * kWave] = lref; sp++; }
+                        else { atomicOr(S.err, 2u); }
+                    }
+                    node = (int)rref;
+                } else if (il) {
+                    node = (int)lref;
+                } else if (sp > 0) {
+                    sp--;
+                    node = (int)my[sp * kWave];
+                } else {
+                    node = -1;
+                }
+            }
+        } else if (kind == 1) {
+            // ------------------------------------------------------------------ LEAF
+            if (wantLeaf) {
+                const uint32_t e = q0;
+                q0 = q1; q1 = q2; q2 = q3;
+                qn--;
+                const int pn = (int)(e >> 1), side = (int)(e & 1u);
+                const float4* np = S.nodes + 4 * (size_t)pn;
+                const float4 a = np[0], b = np[1], q = np[2], r = np[3];
+                const uint32_t ref = __float_as_uint(side ? r.y : r.x);
+                if (slabRec(a, b, q, side, o, inv, 0.001f, closest)) primTest(S, ref, o, d, 0.001f, closest, best, c);
+            }
+        } else {
+            // ------------------------------------------------------------------ SHADE
+            if (wantShade) {
                 bool done = false;
                 float3 contrib = f3(0.0f, 0.0f, 0.0f);
                 if (best < 0) {
@@ -528,69 +585,13 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
                 if (done) {
                     sum = add(sum, contrib);
                     if (++sample == P.spp) {
-                        phase = PH_DONE;
+                        active = false;
                     } else {
                         newPath();
                         beginRay();
                     }
                 } else {
                     beginRay();
-                }
-            }
-        } else if (nL > 0 && (nL >= P.leafBatch || nN == 0)) {
-            // ---------------------------------------------------------------- LEAF
-            if (phase == PH_LEAF) {
-                primTest(S, leafRef, o, d, 0.001f, closest, best, c);
-                if (resumeNode) {
-                    skipLeft = true;
-                    phase = PH_NODE;
-                } else {
-                    popOrShade();
-                }
-            }
-        } else {
-            // ---------------------------------------------------------------- NODE
-            if (phase == PH_NODE) {
-                const float4* np = S.nodes + 4 * (size_t)node;
-                const float4 a = np[0], b = np[1], q = np[2], r = np[3];
-                const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
-                bool toLeaf = false, overflow = false;
-                if (!skipLeft) {
-                    c.visits++;
-                    if (slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest)) {
-                        if (lref & kLeafBit) {
-                            leafRef = lref;
-                            resumeNode = true;
-                            toLeaf = true;
-                        } else if (sp < STACK) {
-                            my[sp * kWave] = lref;
-                            sp++;
-                        } else {
-                            overflow = true;
-                        }
-                    }
-                }
-                if (!toLeaf && !overflow) {
-                    if (slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest)) {
-                        if (rref & kLeafBit) {
-                            leafRef = rref;
-                            resumeNode = false;
-                            toLeaf = true;
-                        } else if (sp < STACK) {
-                            my[sp * kWave] = rref;
-                            sp++;
-                        } else {
-                            overflow = true;
-                        }
-                    }
-                }
-                if (overflow) {
-                    atomicOr(S.err, 2u);
-                    phase = PH_SHADE;
-                } else if (toLeaf) {
-                    phase = PH_LEAF;
-                } else {
-                    popOrShade();
                 }
             }
         }

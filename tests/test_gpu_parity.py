@@ -152,7 +152,12 @@ def test_render_bit_exact(pt, orc, gpu, kernel, name, w, h, spp, depth):
     np.testing.assert_array_equal(bits(rgb), bits(ref))
     np.testing.assert_array_equal(rng_after, ref_states)   # streams advanced identically
     assert st.rays == rst.rays and st.paths == rst.paths == w * h * spp
-    assert st.node_visits == rst.node_visits
+    # the same primitive tests in the same order; speculative traversal may visit extra nodes
+    assert st.tri_tests == rst.tri_tests and st.sphere_tests == rst.sphere_tests
+    if kernel[0] == "simple":
+        assert st.node_visits == rst.node_visits
+    else:
+        assert st.node_visits >= rst.node_visits
 
 
 @pytest.mark.parametrize("w,h,stripe", [(37, 19, 3), (50, 30, 8), (8, 8, 1)])
