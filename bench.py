@@ -69,11 +69,13 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel (0 = the config's)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--leaf-batch", type=int, default=0, help="wavefront LEAF threshold (0 = library default)")
+    ap.add_argument("--shade-batch", type=int, default=0, help="wavefront SHADE threshold (0 = library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,14 +99,22 @@ def main() -> None:
     gathered = torch.empty((world * max_rows * w * 3,), dtype=torch.float32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
-    def frame():
+    def frame(kernel=ptamd.KERNEL_WAVEFRONT):
+        # every step renders the SAME frame: streams back to curand_init(seed, pixel, 0)
+        film.reset(stream.cuda_stream)
         _, st = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
-                             stream=stream.cuda_stream)
+                             stream=stream.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
+                             shade_batch=args.shade_batch)
         if world > 1:
             dist.all_gather_into_tensor(gathered, local_buf)
         return st
 
-    for _ in range(args.warmup):
+    # Warmup 1 uses the ray-synchronous kernel, whose traversal follows the reference's node
+    # order exactly: its counters give the frame's ALGORITHMIC bytes (the wavefront kernel may
+    # visit a few extra nodes speculatively; those are not counted as useful work).  Both
+    # kernels produce the identical frame (same rays, same primitive tests, same pixels).
+    ref_st = frame(ptamd.KERNEL_SIMPLE)
+    for _ in range(max(0, args.warmup - 1)):
         frame()
     if world > 1:
         dist.barrier()
@@ -112,10 +122,14 @@ def main() -> None:
     t0 = time.perf_counter()
     rays = kbytes = 0
     kms = 0.0
+    spec_visits = 0
     for _ in range(args.steps):
         st = frame()
+        if st.rays != ref_st.rays or st.tri_tests != ref_st.tri_tests or st.sphere_tests != ref_st.sphere_tests:
+            raise SystemExit("wavefront frame differs from the reference-order frame")
         rays += st.rays
-        kbytes += st.algo_bytes
+        kbytes += ref_st.algo_bytes
+        spec_visits += st.node_visits
         kms += st.kernel_ms
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -156,8 +170,12 @@ def main() -> None:
                        "rng": "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "renderKernel", "kernel_ms_per_launch": kms / args.steps,
-                         "algo_bytes_per_launch": kbytes / args.steps},
+                         "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
+                         "algo_bytes_per_launch": kbytes / args.steps,
+                         "algo_bytes_source": "reference-order traversal counts of the same frame "
+                                              "(ray-synchronous kernel, warmup step 1)",
+                         "node_visits_reference": ref_st.node_visits,
+                         "node_visits_wavefront": spec_visits / args.steps},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(preset)

@@ -142,6 +142,17 @@ int pt_film_set_rng(pt_film* film, const uint32_t* states);
  * else a host pointer.  The film's RNG streams advance, as the reference's devStates do. */
 int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
               float* out_rgb, int out_on_device, void* stream, pt_stats* stats);
+/* Render options.  kernel: PT_KERNEL_DEFAULT (wavefront unless PT_RENDER_KERNEL=simple),
+ * PT_KERNEL_SIMPLE (ray-synchronous, the reference's loop structure) or PT_KERNEL_WAVEFRONT
+ * (per-lane state machine; steps chosen by wave ballots).  Both give bit-identical images.
+ * leaf_batch / shade_batch: wavefront thresholds in lanes (0 = default). */
+enum { PT_KERNEL_DEFAULT = 0, PT_KERNEL_SIMPLE = 1, PT_KERNEL_WAVEFRONT = 2 };
+typedef struct { int32_t kernel, leaf_batch, shade_batch, reserved; } pt_render_opts;
+int pt_render_ex(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
+                 float* out_rgb, int out_on_device, void* stream, const pt_render_opts* opts,
+                 pt_stats* stats);
+/* Re-initialise the film's streams to their initRandom state (asynchronous on `stream`). */
+int pt_film_reset(pt_film* film, void* stream);
 void pt_film_destroy(pt_film* film);
 void pt_scene_destroy(pt_scene* scene);   /* replaces clearWorldStates (main.cu:451-460) */
 

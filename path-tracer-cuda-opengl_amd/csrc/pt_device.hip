@@ -7,8 +7,8 @@
 //  * traversal: BVH2 whose internal-node record holds BOTH child boxes + child refs (64 B,
 //    four dwordx4 loads per visit, one 64-B segment); leaves are folded into the parent's
 //    child refs; the traversal stack lives in LDS, lane-interleaved (conflict-free).
-//  * primitives are stored in Morton (leaf) order, 48 B each; normals separately (fetched
-//    once per closest hit, not per test).
+//  * primitives are stored in Morton (leaf) order, 48 B each ({v0,v1,v2} / {c,r}: the exact
+//    object box is recomputed from them); normals separately (read once per closest hit).
 //  * LBVH: Karras hierarchy kernel + atomic-counter bottom-up refit with tight boxes.
 // All arithmetic follows the reference's operation order and is compiled with
 // -ffp-contract=off, so results are bit-identical to oracle/ (the CPU restatement).
@@ -114,46 +114,82 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
     return !(hi < lo);
 }
 
-// CudaObj::hit (cuda_object.h:44-92) for the primitive in leaf slot `ref`; on acceptance
-// updates closest/best.  Triangle edges e1 = v1-v0, e2 = v2-v0 are precomputed (same values).
-__device__ __forceinline__ void primTest(const DevScene& S, uint32_t ref, float3 o, float3 d, float tmin,
-                                         float& closest, int& best, Counters& c) {
-    const uint32_t k = ref & kPrimMask;
+// Primitive record (leaf order), 3 x float4:
+//   triangle {v0, mat} {v1, objID} {v2, 0}        sphere {c, mat} {r, 0, 0, objID} {0, 0, 0, 1}
+struct Prim { float4 p0, p1, p2; };
+__device__ __forceinline__ Prim loadPrim(const DevScene& S, uint32_t k) {
     const float4* p = S.prims + 3 * (size_t)k;
-    if (ref & kSphereBit) {
-        c.spheres++;
-        float4 p0 = p[0], p1 = p[1];
-        float3 oc = sub(o, xyz(p0));
-        float r = p1.x;
+    return Prim{p[0], p[1], p[2]};
+}
+
+// Exact object box (cuda_object.h:21-42: sphere c -/+ |r|; triangle via utils::unionPoints)
+// tested like aabb::hit: used to re-test a queued leaf against the current closest hit.
+__device__ __forceinline__ bool primBoxHit(const Prim& q, bool sphere, float3 o, float3 inv, float tmin, float tmax) {
+    if (sphere) {
+        const float r = fabsf(q.p1.x);
+        return slab(q.p0.x - r, q.p0.y - r, q.p0.z - r, q.p0.x + r, q.p0.y + r, q.p0.z + r, o, inv, tmin, tmax);
+    }
+    float mnx = q.p0.x, mny = q.p0.y, mnz = q.p0.z, mxx = mnx, mxy = mny, mxz = mnz;
+    if (mnx > q.p1.x) mnx = q.p1.x;
+    if (mny > q.p1.y) mny = q.p1.y;
+    if (mnz > q.p1.z) mnz = q.p1.z;
+    if (mnx > q.p2.x) mnx = q.p2.x;
+    if (mny > q.p2.y) mny = q.p2.y;
+    if (mnz > q.p2.z) mnz = q.p2.z;
+    if (mxx < q.p1.x) mxx = q.p1.x;
+    if (mxy < q.p1.y) mxy = q.p1.y;
+    if (mxz < q.p1.z) mxz = q.p1.z;
+    if (mxx < q.p2.x) mxx = q.p2.x;
+    if (mxy < q.p2.y) mxy = q.p2.y;
+    if (mxz < q.p2.z) mxz = q.p2.z;
+    return slab(mnx, mny, mnz, mxx, mxy, mxz, o, inv, tmin, tmax);
+}
+
+// CudaObj::hit (cuda_object.h:44-92): returns the accepted t (> tmin > 0), or -1 on a miss.
+// `closest` is the current t_max.  Values are returned, never written through references, so
+// the compiler keeps every traversal variable in registers.
+__device__ __forceinline__ float primHitT(const Prim& q, bool sphere, float3 o, float3 d, float tmin, float closest) {
+    if (sphere) {
+        float3 oc = sub(o, xyz(q.p0));
+        float r = q.p1.x;
         float a = len2(d);
         float half_b = dot3(oc, d);
         float cc = len2(oc) - r * r;
         float disc = half_b * half_b - a * cc;
-        if (disc < 0.0f) return;
+        if (disc < 0.0f) return -1.0f;
         float sq = sqrtf(disc);
         float root = (-half_b - sq) / a;
         if (root < tmin || closest < root) {
             root = (-half_b + sq) / a;
-            if (root < tmin || closest < root) return;
+            if (root < tmin || closest < root) return -1.0f;
         }
-        closest = root;
-        best = (int)k;
-    } else {
-        c.tris++;
-        float4 p0 = p[0], p1 = p[1], p2 = p[2];
-        float3 e1 = xyz(p1), e2 = xyz(p2);
-        float3 s1 = cross3(d, e2);
-        float det = dot3(s1, e1);
-        if (det == 0.0f) return;
-        float3 s = sub(o, xyz(p0));
-        float3 s2 = cross3(s, e1);
-        float inv = 1.0f / det;
-        float t = dot3(s2, e2) * inv;
-        float b1 = dot3(s1, s) * inv;
-        float b2 = dot3(s2, d) * inv;
-        if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 <= 0.0f || b1 + b2 >= 1.0f ||
-            t <= tmin || t >= closest)
-            return;
+        return root;
+    }
+    const float3 v0 = xyz(q.p0);
+    float3 e1 = sub(xyz(q.p1), v0), e2 = sub(xyz(q.p2), v0);
+    float3 s1 = cross3(d, e2);
+    float det = dot3(s1, e1);
+    if (det == 0.0f) return -1.0f;
+    float3 s = sub(o, v0);
+    float3 s2 = cross3(s, e1);
+    float inv = 1.0f / det;
+    float t = dot3(s2, e2) * inv;
+    float b1 = dot3(s1, s) * inv;
+    float b2 = dot3(s2, d) * inv;
+    if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 <= 0.0f || b1 + b2 >= 1.0f ||
+        t <= tmin || t >= closest)
+        return -1.0f;
+    return t;
+}
+
+__device__ __forceinline__ void primTest(const DevScene& S, uint32_t ref, float3 o, float3 d, float tmin,
+                                         float& closest, int& best, Counters& c) {
+    const uint32_t k = ref & kPrimMask;
+    const bool sph = (ref & kSphereBit) != 0;
+    if (sph) c.spheres++;
+    else c.tris++;
+    const float t = primHitT(loadPrim(S, k), sph, o, d, tmin, closest);
+    if (t >= 0.0f) {
         closest = t;
         best = (int)k;
     }
@@ -431,14 +467,8 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 // so primitive tests run with many lanes active instead of one or two.
 constexpr int kLeafQ = 4;
 
-__device__ __forceinline__ bool slabRec(const float4& a, const float4& b, const float4& q, int side, float3 o,
-                                        float3 inv, float tmin, float tmax) {
-    return side == 0 ? slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, tmax)
-                     : slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, tmin, tmax);
-}
-
 template <int STACK>
-__global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
     const int tile = xcdTile(blockIdx.x, P.ntiles);
@@ -451,8 +481,9 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
     const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
     uint32_t* my = stk + lane;
-    Counters c{0, 0, 0, 0};
-    uint32_t paths = 0;
+    // Work counters are wave totals kept in scalar registers: each step adds the popcount of
+    // a ballot of the lanes that did the work (no per-lane counter VGPRs).
+    uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
 
     Xorwow g{0, 0, 0, 0, 0, 0};
     if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
@@ -460,46 +491,54 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
     int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
-    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: (parent node << 1) | side
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: leaf refs in DFS order
     bool active = false;
 
-    auto beginRay = [&]() {   // start the closest-hit query of (o, d)
-        c.rays++;
-        depthLeft--;
-        closest = __builtin_inff();
-        best = -1;
-        sp = 0;
-        qn = 0;
-        if (S.nprims <= 1) {
-            node = -1;
-            if (S.nprims == 1) {   // root is a leaf: tested without a box test (render_manager.h:92-98)
-                const uint32_t ref = kLeafBit | (__float_as_uint(S.prims[2].w) ? kSphereBit : 0u);
-                primTest(S, ref, o, d, 0.001f, closest, best, c);
-            }
-        } else {
-            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-            node = 0;
-        }
-    };
-    auto newPath = [&]() {   // main.cu:284-286 + camera::get_ray (lens/time draws skipped)
-        float u = (fcol + g.uniform()) * P.invW;
-        float v = (frow + g.uniform()) * P.invH;
-        o = P.cam.pos;
-        d = sub(add(add(P.cam.ll, scale(u, P.cam.hor)), scale(v, P.cam.ver)), P.cam.pos);
-        att = f3(1.0f, 1.0f, 1.0f);
-        depthLeft = P.max_depth;
-        paths++;
-    };
+    // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
+    // captured variables address-taken and they end up in scratch memory.)
+#define PT_BEGIN_RAY()                                                                              \
+    do {                                                                                          \
+        depthLeft--;                                                                              \
+        closest = __builtin_inff();                                                               \
+        best = -1;                                                                                \
+        sp = 0;                                                                                   \
+        qn = 0;                                                                                   \
+        if (S.nprims <= 1) {                                                                      \
+            node = -1;                                                                            \
+            if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
+                const float t1 = primHitT(loadPrim(S, 0), __float_as_uint(S.prims[2].w) != 0, o, d, \
+                                          0.001f, closest);                                       \
+                if (t1 >= 0.0f) { closest = t1; best = 0; }                                       \
+            }                                                                                     \
+        } else {                                                                                  \
+            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
+            node = 0;                                                                             \
+        }                                                                                         \
+    } while (0)
+    // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
+#define PT_NEW_PATH()                                                                               \
+    do {                                                                                          \
+        const float u_ = (fcol + g.uniform()) * P.invW;                                           \
+        const float v_ = (frow + g.uniform()) * P.invH;                                           \
+        o = P.cam.pos;                                                                            \
+        d = sub(add(add(P.cam.ll, scale(u_, P.cam.hor)), scale(v_, P.cam.ver)), P.cam.pos);       \
+        att = f3(1.0f, 1.0f, 1.0f);                                                               \
+        depthLeft = P.max_depth;                                                                  \
+    } while (0)
 
+    bool started = false;
     if (valid) {
         if (P.max_depth <= 0) {
-            for (; sample < P.spp; sample++) { newPath(); sum = add(sum, sky(d, att)); }
+            for (; sample < P.spp; sample++) { PT_NEW_PATH(); sum = add(sum, sky(d, att)); }
         } else if (P.spp > 0) {
-            newPath();
-            beginRay();
+            PT_NEW_PATH();
+            PT_BEGIN_RAY();
             active = true;
+            started = true;
         }
     }
+    sRays += (uint32_t)__popcll(__ballot(started));
+    sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)P.spp : 0u);
 
     for (;;) {
         const bool wantNode = node >= 0 && qn <= kLeafQ - 2;
@@ -516,22 +555,20 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
 
         if (kind == 0) {
             // ------------------------------------------------------------------ NODE
+            sVisits += (uint32_t)nN;
             if (wantNode) {
-                c.visits++;
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
                 const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
                 const bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest);
                 const bool hr = slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest);
-                const uint32_t e0 = (uint32_t)node << 1;
                 // append hit leaves in order (left, then right)
                 if (hl && (lref & kLeafBit)) {
-                    q0 = qn == 0 ? e0 : q0; q1 = qn == 1 ? e0 : q1; q2 = qn == 2 ? e0 : q2; q3 = qn == 3 ? e0 : q3;
+                    q0 = qn == 0 ? lref : q0; q1 = qn == 1 ? lref : q1; q2 = qn == 2 ? lref : q2; q3 = qn == 3 ? lref : q3;
                     qn++;
                 }
                 if (hr && (rref & kLeafBit)) {
-                    const uint32_t e1 = e0 | 1u;
-                    q0 = qn == 0 ? e1 : q0; q1 = qn == 1 ? e1 : q1; q2 = qn == 2 ? e1 : q2; q3 = qn == 3 ? e1 : q3;
+                    q0 = qn == 0 ? rref : q0; q1 = qn == 1 ? rref : q1; q2 = qn == 2 ? rref : q2; q3 = qn == 3 ? rref : q3;
                     qn++;
                 }
                 const bool il = hl && !(lref & kLeafBit), ir = hr && !(rref & kLeafBit);
@@ -553,18 +590,25 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
             }
         } else if (kind == 1) {
             // ------------------------------------------------------------------ LEAF
+            bool tested = false, sph = false;
             if (wantLeaf) {
-                const uint32_t e = q0;
+                const uint32_t ref = q0;
                 q0 = q1; q1 = q2; q2 = q3;
                 qn--;
-                const int pn = (int)(e >> 1), side = (int)(e & 1u);
-                const float4* np = S.nodes + 4 * (size_t)pn;
-                const float4 a = np[0], b = np[1], q = np[2], r = np[3];
-                const uint32_t ref = __float_as_uint(side ? r.y : r.x);
-                if (slabRec(a, b, q, side, o, inv, 0.001f, closest)) primTest(S, ref, o, d, 0.001f, closest, best, c);
+                const uint32_t k = ref & kPrimMask;
+                sph = (ref & kSphereBit) != 0;
+                const Prim pr = loadPrim(S, k);
+                if (primBoxHit(pr, sph, o, inv, 0.001f, closest)) {
+                    tested = true;
+                    const float t = primHitT(pr, sph, o, d, 0.001f, closest);
+                    if (t >= 0.0f) { closest = t; best = (int)k; }
+                }
             }
+            sTris += (uint32_t)__popcll(__ballot(tested && !sph));
+            sSph += (uint32_t)__popcll(__ballot(tested && sph));
         } else {
             // ------------------------------------------------------------------ SHADE
+            bool newRay = false, newSample = false;
             if (wantShade) {
                 bool done = false;
                 float3 contrib = f3(0.0f, 0.0f, 0.0f);
@@ -587,13 +631,17 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
                     if (++sample == P.spp) {
                         active = false;
                     } else {
-                        newPath();
-                        beginRay();
+                        PT_NEW_PATH();
+                        PT_BEGIN_RAY();
+                        newRay = newSample = true;
                     }
                 } else {
-                    beginRay();
+                    PT_BEGIN_RAY();
+                    newRay = true;
                 }
             }
+            sRays += (uint32_t)__popcll(__ballot(newRay));
+            sPaths += (uint32_t)__popcll(__ballot(newSample));
         }
     }
     if (valid) {
@@ -603,12 +651,16 @@ __global__ __launch_bounds__(kWave) void renderKernelWF(RenderParams P) {
         outp[2] = sqrtf(sum.z * P.invSpp);
         P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
     }
-    waveReduceAdd(P.counters + 0, c.rays);
-    waveReduceAdd(P.counters + 1, c.visits);
-    waveReduceAdd(P.counters + 2, c.tris);
-    waveReduceAdd(P.counters + 3, c.spheres);
-    waveReduceAdd(P.counters + 4, paths);
+    if (lane == 0) {
+        atomicAdd(P.counters + 0, (unsigned long long)sRays);
+        atomicAdd(P.counters + 1, (unsigned long long)sVisits);
+        atomicAdd(P.counters + 2, (unsigned long long)sTris);
+        atomicAdd(P.counters + 3, (unsigned long long)sSph);
+        atomicAdd(P.counters + 4, (unsigned long long)sPaths);
+    }
 }
+#undef PT_BEGIN_RAY
+#undef PT_NEW_PATH
 
 template <int STACK>
 __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* rays, int64_t n, float tmin,
@@ -860,7 +912,9 @@ struct pt_film {
     int width = 0, height = 0, stripe_h = 1, nparts = 1, part = 0;
     int nrows = 0;
     int64_t npix = 0;
+    uint64_t seed = 0;
     DevBuf state;   // 6 x npix uint32 (SoA)
+    DevBuf jumps;   // XORWOW jump matrices (for pt_film_reset)
 };
 
 namespace {
@@ -901,6 +955,18 @@ int dispatchTrace(int stack, const DevScene& S, const pt_ray* r, int64_t n, floa
         case 80: traceKernel<80><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
         default: return fail(PT_ERR_STATE, "unsupported BVH depth");
     }
+    HIP_TRY(hipGetLastError());
+    return PT_OK;
+}
+
+// (Re)initialise every stream of the film to curand_init(seed, pixel, 0), asynchronously.
+int filmInit(pt_film* f, hipStream_t st) {
+    if (f->npix <= 0) return PT_OK;
+    uint32_t* b = f->state.as<uint32_t>();
+    const int64_t np = f->npix;
+    rngInitKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(b, b + np, b + 2 * np, b + 3 * np, b + 4 * np, b + 5 * np,
+                                                                 f->jumps.as<uint32_t>(), f->seed, f->width, f->nrows,
+                                                                 f->stripe_h, f->nparts, f->part);
     HIP_TRY(hipGetLastError());
     return PT_OK;
 }
@@ -1001,11 +1067,10 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
             sphereFlag[k] = 1;
         } else {
             const pt::vec3 v0(o.v[0], o.v[1], o.v[2]), v1(o.v[3], o.v[4], o.v[5]), v2(o.v[6], o.v[7], o.v[8]);
-            const pt::vec3 e1 = v1 - v0, e2 = v2 - v0;
             const pt::vec3 nn = pt::normalize(pt::cross(v1 - v0, v2 - v0));   // triangle.h:17-19
             prims[3 * k] = make_float4(v0.x(), v0.y(), v0.z(), bits((uint32_t)o.mat));
-            prims[3 * k + 1] = make_float4(e1.x(), e1.y(), e1.z(), bits(id));
-            prims[3 * k + 2] = make_float4(e2.x(), e2.y(), e2.z(), bits(0u));
+            prims[3 * k + 1] = make_float4(v1.x(), v1.y(), v1.z(), bits(id));
+            prims[3 * k + 2] = make_float4(v2.x(), v2.y(), v2.z(), bits(0u));
             normals[k] = make_float4(nn.x(), nn.y(), nn.z(), 0.0f);
             for (int a = 0; a < 3; a++) {
                 float mn = o.v[a], mx = o.v[a];
@@ -1187,20 +1252,21 @@ int pt_film_create(int device, int width, int height, int sh, int nparts, int pa
     f->nrows = rows;
     f->npix = (int64_t)rows * width;
     if ((rc = devAlloc(f->state, (size_t)std::max<int64_t>(1, f->npix) * 6 * 4))) return rc;
-    if (f->npix > 0) {
-        const std::vector<uint32_t>& jm = jumpMatrices();
-        DevBuf djm;
-        if ((rc = devAlloc(djm, jm.size() * 4))) return rc;
-        HIP_TRY(hipMemcpy(djm.p, jm.data(), jm.size() * 4, hipMemcpyHostToDevice));
-        uint32_t* b = f->state.as<uint32_t>();
-        const int64_t np = f->npix;
-        rngInitKernel<<<(unsigned)((np + 255) / 256), 256>>>(b, b + np, b + 2 * np, b + 3 * np, b + 4 * np, b + 5 * np,
-                                                               djm.as<uint32_t>(), seed, width, rows, sh, nparts, part);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipDeviceSynchronize());
-    }
+    f->seed = seed;
+    const std::vector<uint32_t>& jm = jumpMatrices();
+    if ((rc = devAlloc(f->jumps, jm.size() * 4))) return rc;
+    HIP_TRY(hipMemcpy(f->jumps.p, jm.data(), jm.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = filmInit(f.get(), 0))) return rc;
+    HIP_TRY(hipDeviceSynchronize());
     *out = f.release();
     return PT_OK;
+}
+
+int pt_film_reset(pt_film* f, void* stream) {
+    if (!f) return fail(PT_ERR_INVALID, "pt_film_reset: null film");
+    int rc = setDevice(f->device);
+    if (rc) return rc;
+    return filmInit(f, (hipStream_t)stream);
 }
 
 int pt_film_info(pt_film* f, int* nrows, int64_t* npix) {
@@ -1244,6 +1310,11 @@ int pt_film_set_rng(pt_film* f, const uint32_t* states) {
 
 int pt_render(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_depth, float* out, int on_dev,
               void* stream, pt_stats* stats) {
+    return pt_render_ex(s, f, cam, spp, max_depth, out, on_dev, stream, nullptr, stats);
+}
+
+int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_depth, float* out, int on_dev,
+                 void* stream, const pt_render_opts* opts, pt_stats* stats) {
     if (!s || !f || !cam || !out || spp <= 0) return fail(PT_ERR_INVALID, "pt_render: bad argument");
     if (!s->built) return fail(PT_ERR_STATE, "pt_render: BVH not built");
     if (s->device != f->device) return fail(PT_ERR_INVALID, "pt_render: scene and film on different devices");
@@ -1283,13 +1354,18 @@ int pt_render(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_de
     P.invW = 1.0f / (float)f->width;    // main.cu:281
     P.invH = 1.0f / (float)f->height;
     P.invSpp = 1.0f / (float)spp;
-    // Scheduler: PT_RENDER_KERNEL=simple selects the ray-synchronous kernel; PT_LEAF_BATCH /
-    // PT_SHADE_BATCH tune the wavefront kernel's step thresholds (lanes out of 64).
-    P.leafBatch = envInt("PT_LEAF_BATCH", 16);
-    P.shadeBatch = envInt("PT_SHADE_BATCH", 24);
-    if (const char* k = std::getenv("PT_RENDER_KERNEL")) {
-        if (std::string(k) == "simple") P.leafBatch = 0;
+    // Kernel choice and wavefront-scheduler thresholds (lanes of 64): explicit options win, then
+    // the PT_RENDER_KERNEL / PT_LEAF_BATCH / PT_SHADE_BATCH environment (tuning), then defaults.
+    int kernel = opts ? opts->kernel : PT_KERNEL_DEFAULT;
+    if (kernel == PT_KERNEL_DEFAULT) {
+        const char* k = std::getenv("PT_RENDER_KERNEL");
+        kernel = (k && std::string(k) == "simple") ? PT_KERNEL_SIMPLE : PT_KERNEL_WAVEFRONT;
     }
+    if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT)
+        return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
+    P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64) : envInt("PT_LEAF_BATCH", 8);
+    P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64) : envInt("PT_SHADE_BATCH", 16);
+    if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
     const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));

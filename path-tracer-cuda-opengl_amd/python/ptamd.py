@@ -50,6 +50,13 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class RenderOpts(C.Structure):
+    _fields_ = [("kernel", C.c_int32), ("leaf_batch", C.c_int32), ("shade_batch", C.c_int32), ("reserved", C.c_int32)]
+
+
+KERNEL_DEFAULT, KERNEL_SIMPLE, KERNEL_WAVEFRONT = 0, 1, 2
+
+
 class SceneDesc(C.Structure):
     _fields_ = [("objects", C.c_void_p), ("n_objects", C.c_int64), ("materials", C.c_void_p),
                 ("n_materials", C.c_int64), ("camera", Camera), ("width", C.c_int32), ("height", C.c_int32),
@@ -62,7 +69,7 @@ EXPORTS = [
     "pt_preset_scene", "pt_scene_desc_free", "pt_load_obj", "pt_free", "pt_morton_keys", "pt_write_png",
     "pt_quantize_rgba8", "pt_scene_create", "pt_scene_build_bvh", "pt_scene_bvh_info", "pt_scene_download_bvh",
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
-    "pt_render", "pt_film_destroy", "pt_scene_destroy",
+    "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -96,6 +103,9 @@ _sig = {
     "pt_film_get_rng": (C.c_int, [_P, _P]),
     "pt_film_set_rng": (C.c_int, [_P, _P]),
     "pt_render": (C.c_int, [_P, _P, C.POINTER(Camera), C.c_int, C.c_int, _P, C.c_int, _P, C.POINTER(Stats)]),
+    "pt_render_ex": (C.c_int, [_P, _P, C.POINTER(Camera), C.c_int, C.c_int, _P, C.c_int, _P, C.POINTER(RenderOpts),
+                               C.POINTER(Stats)]),
+    "pt_film_reset": (C.c_int, [_P, _P]),
     "pt_film_destroy": (None, [_P]),
     "pt_scene_destroy": (None, [_P]),
 }
@@ -268,6 +278,10 @@ class Film:
         assert states.shape == (self.n_pixels, 6)
         _check(lib.pt_film_set_rng(self.h, _ptr(states)), "pt_film_set_rng")
 
+    def reset(self, stream=None) -> None:
+        """Back to the initRandom state: curand_init(seed, pixel, 0) for every pixel."""
+        _check(lib.pt_film_reset(self.h, C.c_void_p(int(stream) if stream else 0)), "pt_film_reset")
+
     def close(self) -> None:
         if self.h:
             lib.pt_film_destroy(self.h)
@@ -280,16 +294,18 @@ class Film:
             pass
 
 
-def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, out=None, stream=None):
+def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, out=None, stream=None,
+           kernel: int = KERNEL_DEFAULT, leaf_batch: int = 0, shade_batch: int = 0):
     """Render spp samples per pixel of the film's rows.  `out` may be a numpy array (host) or
     an integer device pointer (then `stream` is a hipStream_t handle or None).  Returns
     (rgb or None, Stats)."""
     st = Stats()
+    opts = RenderOpts(kernel, leaf_batch, shade_batch, 0)
     if out is None or isinstance(out, np.ndarray):
         rgb = out if out is not None else np.zeros((film.n_pixels, 3), np.float32)
-        _check(lib.pt_render(scene.h, film.h, C.byref(camera), spp, max_depth, _ptr(rgb), 0, None, C.byref(st)),
-               "pt_render")
+        _check(lib.pt_render_ex(scene.h, film.h, C.byref(camera), spp, max_depth, _ptr(rgb), 0, None, C.byref(opts),
+                                C.byref(st)), "pt_render_ex")
         return rgb, st
-    _check(lib.pt_render(scene.h, film.h, C.byref(camera), spp, max_depth, C.c_void_p(int(out)), 1,
-                         C.c_void_p(int(stream) if stream else 0), C.byref(st)), "pt_render")
+    _check(lib.pt_render_ex(scene.h, film.h, C.byref(camera), spp, max_depth, C.c_void_p(int(out)), 1,
+                            C.c_void_p(int(stream) if stream else 0), C.byref(opts), C.byref(st)), "pt_render_ex")
     return None, st

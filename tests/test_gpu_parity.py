@@ -277,3 +277,21 @@ print("ok", st.rays)
                          "python")
     r = subprocess.run([sys.executable, "-c", code, pydir], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_film_reset_and_explicit_kernels(pt, gpu):
+    """pt_film_reset restores curand_init streams; both kernels (explicit options) give the
+    identical frame from the same initial streams."""
+    w, h = 96, 54
+    p = pt.Preset("bunny_cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, 4, device=gpu)
+    init = f.get_rng()
+    a, sa = pt.render(s, f, p.camera, 3, 50, kernel=pt.KERNEL_SIMPLE)
+    f.reset()
+    np.testing.assert_array_equal(f.get_rng(), init)
+    b, sb = pt.render(s, f, p.camera, 3, 50, kernel=pt.KERNEL_WAVEFRONT, leaf_batch=9, shade_batch=33)
+    np.testing.assert_array_equal(bits(a), bits(b))
+    assert sa.rays == sb.rays and sa.tri_tests == sb.tri_tests
+    with pytest.raises(pt.PtError):
+        pt.render(s, f, p.camera, 1, 5, kernel=7)
