@@ -349,6 +349,7 @@ struct RenderParams {
     int spp, max_depth;
     float invW, invH, invSpp;
     int leafBatch, shadeBatch;                // wavefront scheduler thresholds (lanes)
+    unsigned long long* waveTimes;            // optional (PT_WAVE_TIMES): {start, end, tile|xcc<<32} per wave
 };
 
 __device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
@@ -477,6 +478,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     const int lrow = ty * 8 + (lane >> 3);
     const bool valid = col < P.width && lrow < P.nrows;
     const size_t idx = valid ? (size_t)lrow * P.width + col : 0;
+    const unsigned long long tStart = P.waveTimes ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const float fcol = (float)col;
     const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
@@ -650,6 +652,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         outp[1] = sqrtf(sum.y * P.invSpp);
         outp[2] = sqrtf(sum.z * P.invSpp);
         P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+    }
+    if (P.waveTimes && lane == 0) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        P.waveTimes[3 * (size_t)blockIdx.x + 0] = tStart;
+        P.waveTimes[3 * (size_t)blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        P.waveTimes[3 * (size_t)blockIdx.x + 2] = (unsigned long long)tile | ((unsigned long long)(xcc & 0xf) << 32);
     }
     if (lane == 0) {
         atomicAdd(P.counters + 0, (unsigned long long)sRays);
@@ -1367,6 +1376,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64) : envInt("PT_SHADE_BATCH", 16);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
     const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
+    DevBuf dtimes;
+    const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
+    P.waveTimes = nullptr;
+    if (timesPath && *timesPath && kernel == PT_KERNEL_WAVEFRONT) {
+        if ((rc = devAlloc(dtimes, (size_t)std::max(1, P.ntiles) * 24))) return rc;
+        HIP_TRY(hipMemsetAsync(dtimes.p, 0, (size_t)std::max(1, P.ntiles) * 24, st));
+        P.waveTimes = dtimes.as<unsigned long long>();
+    }
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -1381,6 +1398,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    if (P.waveTimes) {
+        std::vector<unsigned long long> t((size_t)P.ntiles * 3);
+        HIP_TRY(hipMemcpy(t.data(), dtimes.p, t.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE* fp = std::fopen(timesPath, "wb")) {
+            std::fwrite(t.data(), 8, t.size(), fp);
+            std::fclose(fp);
+        }
+    }
     if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * 12, hipMemcpyDeviceToHost));
     unsigned long long c[8] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
