@@ -350,18 +350,22 @@ struct RenderParams {
     float invW, invH, invSpp;
     int leafBatch, shadeBatch;                // wavefront scheduler thresholds (lanes)
     unsigned long long* waveTimes;            // optional (PT_WAVE_TIMES): {start, end, tile|xcc<<32} per wave
+    const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
+    unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
+    int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
 };
 
 __device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
     return ((lrow / sh) * nparts + part) * sh + lrow % sh;
 }
 
-// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so
-// give each XCD a contiguous band of tiles (its L2 then holds one band's working set).
-// Bijective: XCD x (= bid % 8) owns q + (x < r) tiles starting at x*q + min(x, r).
-__device__ __forceinline__ int xcdTile(int bid, int ntiles) {
-    const int q = ntiles >> 3, r = ntiles & 7, x = bid & 7;
-    return x * q + min(x, r) + (bid >> 3);
+// Tile scheduling.  Workgroups are dispatched in blockIdx order and dealt round-robin over the 8
+// XCDs, so consecutive tiles land on different XCDs (balanced; the C3 BVH fits every L2).  When
+// the film has measured per-tile costs from a previous launch, tiles are launched longest first
+// (LPT): a tile's 1024 samples per pixel are sequential (per-pixel RNG stream), so the most
+// expensive tiles are the critical path and must start first.  Scheduling never changes results.
+__device__ __forceinline__ int tileOf(const RenderParams& P, int bid) {
+    return P.tileOrder ? P.tileOrder[bid] : bid;
 }
 
 __device__ __forceinline__ void waveReduceAdd(unsigned long long* dst, uint32_t v) {
@@ -375,7 +379,8 @@ template <int STACK>
 __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
-    const int tile = xcdTile(blockIdx.x, P.ntiles);
+    const int tile = tileOf(P, blockIdx.x);
+    const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int col = tx * 8 + (lane & 7);
     const int lrow = ty * 8 + (lane >> 3);
@@ -441,6 +446,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
         outp[2] = sqrtf(sum.z * P.invSpp);
         P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
     }
+    if (lane == 0) P.tileCost[tile] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - tStart, 0xffffffffull);
     waveReduceAdd(P.counters + 0, c.rays);
     waveReduceAdd(P.counters + 1, c.visits);
     waveReduceAdd(P.counters + 2, c.tris);
@@ -472,13 +478,14 @@ template <int STACK>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
-    const int tile = xcdTile(blockIdx.x, P.ntiles);
+    const int tile = tileOf(P, blockIdx.x);
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int col = tx * 8 + (lane & 7);
     const int lrow = ty * 8 + (lane >> 3);
     const bool valid = col < P.width && lrow < P.nrows;
     const size_t idx = valid ? (size_t)lrow * P.width + col : 0;
-    const unsigned long long tStart = P.waveTimes ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
+    if ((int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
     const float fcol = (float)col;
     const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
@@ -653,11 +660,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         outp[2] = sqrtf(sum.z * P.invSpp);
         P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
     }
+    const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
     if (P.waveTimes && lane == 0) {
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         P.waveTimes[3 * (size_t)blockIdx.x + 0] = tStart;
-        P.waveTimes[3 * (size_t)blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        P.waveTimes[3 * (size_t)blockIdx.x + 1] = tEnd;
         P.waveTimes[3 * (size_t)blockIdx.x + 2] = (unsigned long long)tile | ((unsigned long long)(xcc & 0xf) << 32);
     }
     if (lane == 0) {
@@ -924,6 +933,8 @@ struct pt_film {
     uint64_t seed = 0;
     DevBuf state;   // 6 x npix uint32 (SoA)
     DevBuf jumps;   // XORWOW jump matrices (for pt_film_reset)
+    DevBuf tileCost, tileOrder;   // measured per-tile cost of the last launch; LPT launch order
+    bool haveOrder = false;
 };
 
 namespace {
@@ -1376,6 +1387,15 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64) : envInt("PT_SHADE_BATCH", 16);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
     const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
+    const size_t ntl = (size_t)std::max(1, P.ntiles);
+    if (!f->tileCost.p) {
+        if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4))) return rc;
+        f->haveOrder = false;
+    }
+    const bool lpt = !(opts && opts->reserved == 1);   // reserved == 1: identity order (A/B)
+    P.tileCost = f->tileCost.as<unsigned>();
+    P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
+    P.prioTiles = P.tileOrder ? envInt("PT_PRIO_TILES", 1024) : 0;
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
@@ -1398,6 +1418,15 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    if (lpt && P.ntiles > 0) {   // next launch: longest tiles first
+        std::vector<unsigned> cost(ntl);
+        HIP_TRY(hipMemcpy(cost.data(), f->tileCost.p, ntl * 4, hipMemcpyDeviceToHost));
+        std::vector<int> order(ntl);
+        for (size_t i = 0; i < ntl; i++) order[i] = (int)i;
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+        HIP_TRY(hipMemcpy(f->tileOrder.p, order.data(), ntl * 4, hipMemcpyHostToDevice));
+        f->haveOrder = true;
+    }
     if (P.waveTimes) {
         std::vector<unsigned long long> t((size_t)P.ntiles * 3);
         HIP_TRY(hipMemcpy(t.data(), dtimes.p, t.size() * 8, hipMemcpyDeviceToHost));

@@ -295,3 +295,19 @@ def test_film_reset_and_explicit_kernels(pt, gpu):
     assert sa.rays == sb.rays and sa.tri_tests == sb.tri_tests
     with pytest.raises(pt.PtError):
         pt.render(s, f, p.camera, 1, 5, kernel=7)
+
+
+def test_lpt_tile_order_is_result_neutral(pt, gpu):
+    """After a first launch the film launches tiles longest-first with raised priority for the
+    head of the order; the frame must be bit-identical to the identity-order launch."""
+    w, h = 160, 90
+    p = pt.Preset("bunny_cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, 21, device=gpu)
+    frames = []
+    for _ in range(3):   # 1st: identity order (no costs yet), 2nd/3rd: LPT from measured costs
+        f.reset()
+        rgb, st = pt.render(s, f, p.camera, 2, 50)
+        frames.append(rgb.copy())
+    for fr in frames[1:]:
+        np.testing.assert_array_equal(bits(fr), bits(frames[0]))
