@@ -53,6 +53,8 @@ for name, res, args in [
     ("orc_bvh_depth", C.c_int, [_P, C.c_int64]),
     ("orc_trace", C.c_int, [_P, C.c_int64, _P, _P, C.c_int64, C.c_float, C.c_float, C.c_int, _P, C.POINTER(Stats)]),
     ("orc_scatter_tape", C.c_int, [_P, _P, _P, _P, C.c_int, C.POINTER(C.c_int), _P, _P]),
+    ("orc_render2", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
+                              C.c_int, _P, _P, C.POINTER(Stats), C.c_int, _P]),
     ("orc_render", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
                              C.c_int, _P, _P, C.POINTER(Stats), C.c_int]),
 ]:
@@ -157,6 +159,21 @@ def render(objects, materials, nodes, camera: np.ndarray, width: int, height: in
     lib.orc_render(_ptr(objects), len(objects), _ptr(materials), len(materials), _ptr(nodes), _ptr(camera), width,
                    height, _ptr(rows), len(rows), spp, max_depth, _ptr(states), _ptr(out), C.byref(st), nthreads)
     return out, st
+
+
+def render_pixel_rays(objects, materials, nodes, camera, width, height, rows, spp, max_depth, states, nthreads=1):
+    """orc_render + per-pixel ray counts: (rgb, rays uint32 (npix,), Stats)."""
+    objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+    materials = np.ascontiguousarray(materials, MATERIAL_DTYPE)
+    rows = np.ascontiguousarray(rows, np.int32)
+    camera = np.ascontiguousarray(camera, np.float32)
+    out = np.zeros((len(rows) * width, 3), np.float32)
+    cnt = np.zeros(len(rows) * width, np.uint32)
+    st = Stats()
+    lib.orc_render2(_ptr(objects), len(objects), _ptr(materials), len(materials), _ptr(nodes), _ptr(camera), width,
+                    height, _ptr(rows), len(rows), spp, max_depth, _ptr(states), _ptr(out), C.byref(st), nthreads,
+                    _ptr(cnt))
+    return out, cnt, st
 
 
 def film_states(seed: int, width: int, rows) -> np.ndarray:

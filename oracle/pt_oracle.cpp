@@ -595,9 +595,20 @@ int orc_scatter_tape(const orc_material* m, const float ray[6], const orc_hit* r
     return ok ? 1 : 0;
 }
 
+int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
+                const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
+                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays);
+
 int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
                const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads) {
+    return orc_render2(objs, nobj, mats, nmat, nodes, cam, width, height, rows, nrows, spp, max_depth, states, out_rgb,
+                       stats, nthreads, nullptr);
+}
+
+int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
+                const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
+                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays) {
     (void)nmat; (void)height;
     if (nthreads < 1) nthreads = 1;
     const V3 pos = load3(cam->origin), ll = load3(cam->lower_left);
@@ -616,6 +627,7 @@ int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, i
                 uint32_t* s = states + 6 * k;
                 XorwowRng rng{s};
                 V3 sum{0, 0, 0};
+                const uint64_t rays0 = local.rays;
                 for (int i = 0; i < spp; i++) {                                        // main.cu:283-289
                     float u = ((float)col + curandUniform(s)) * invW;
                     float v = ((float)row + curandUniform(s)) * invH;
@@ -647,6 +659,7 @@ int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, i
                     }
                     sum = sum + c;                                                      // vec3::operator+=
                 }
+                if (pixel_rays) pixel_rays[k] = (uint32_t)(local.rays - rays0);
                 out_rgb[3 * k + 0] = std::sqrt(sum.x * invSpp);                        // main.cu:290-293
                 out_rgb[3 * k + 1] = std::sqrt(sum.y * invSpp);
                 out_rgb[3 * k + 2] = std::sqrt(sum.z * invSpp);

@@ -71,6 +71,12 @@ int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, i
                const int32_t* rows, int nrows, int spp, int max_depth,
                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads);
 
+/* orc_render plus per-pixel ray counts (diagnostics). */
+int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
+                const orc_node* nodes, const orc_camera* cam, int width, int height,
+                const int32_t* rows, int nrows, int spp, int max_depth,
+                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays);
+
 #ifdef __cplusplus
 }
 #endif

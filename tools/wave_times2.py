@@ -15,8 +15,7 @@ from wave_times import analyse  # noqa: E402
 p = ptamd.Preset("bunny_cornell")
 scene = ptamd.Scene(p.objects, p.materials)
 film = ptamd.Film(p.width, p.height, 1)
-for label, prio in (("identity", "0"), ("lpt_noprio", "0"), ("lpt_prio1024", "1024"), ("lpt_prio4096", "4096"),
-                    ("lpt_prio256", "256")):
+for label, prio in (("identity", "0"), ("lpt_noprio", "0"), ("lpt_prio1024", "1024")):
     out = os.path.join(REPO, "gpurun_out", f"wt_{label}.bin")
     os.environ.update(PT_WAVE_TIMES=out, PT_PRIO_TILES=prio)
     film.reset()
