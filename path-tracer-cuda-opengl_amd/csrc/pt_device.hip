@@ -556,15 +556,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
-        // Thresholds scale with the lanes still rendering, so the last lanes of a wave (the
-        // pixels with the longest sample chains: the frame's critical path) never wait for a
-        // batch that cannot fill.
-        const int nAct = __popcll(__ballot(active));
-        const int tl = max(1, (P.leafBatch * nAct) >> 6), ts = max(1, (P.shadeBatch * nAct) >> 6);
         int kind;   // 0 node, 1 leaf, 2 shade
         if (nN == 0) kind = nL > 0 ? 1 : 2;
-        else if (nL >= tl) kind = 1;
-        else if (nS >= ts) kind = 2;
+        else if (nL >= P.leafBatch) kind = 1;
+        else if (nS >= P.shadeBatch) kind = 2;
         else kind = 0;
 
         if (kind == 0) {
