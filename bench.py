@@ -99,7 +99,7 @@ def main() -> None:
     gathered = torch.empty((world * max_rows * w * 3,), dtype=torch.float32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
-    def frame(kernel=ptamd.KERNEL_WAVEFRONT):
+    def frame(kernel=ptamd.KERNEL_DEFAULT):
         # every step renders the SAME frame: streams back to curand_init(seed, pixel, 0)
         film.reset(stream.cuda_stream)
         _, st = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
@@ -170,7 +170,7 @@ def main() -> None:
                        "rng": "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
+                         "kernel": "renderKernelW4", "kernel_ms_per_launch": kms / args.steps,
                          "algo_bytes_per_launch": kbytes / args.steps,
                          "algo_bytes_source": "reference-order traversal counts of the same frame "
                                               "(ray-synchronous kernel, warmup step 1)",

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <string>
 #include <vector>
@@ -50,6 +51,7 @@ struct DevScene {
     const float4* prims;     // 3 x float4 per primitive (leaf order)
     const float4* normals;   // 1 x float4 per primitive (triangles)
     const float4* mats;      // 2 x float4 per material
+    const float4* wnodes;    // 4-wide nodes, 8 x float4 each (see renderKernelW4)
     unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
     int nprims;
 };
@@ -349,6 +351,7 @@ struct RenderParams {
     int spp, max_depth;
     float invW, invH, invSpp;
     int leafBatch, shadeBatch;                // wavefront scheduler thresholds (lanes)
+    int kernel;                               // PT_KERNEL_*
     unsigned long long* waveTimes;            // optional (PT_WAVE_TIMES): {start, end, tile|xcc<<32} per wave
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
@@ -680,6 +683,246 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
 #undef PT_BEGIN_RAY
 #undef PT_NEW_PATH
 
+// 4-wide variant of renderKernelWF.  Wide node (128 B = 8 x float4): SoA child boxes
+// {minx[4]}{miny[4]}{minz[4]}{maxx[4]}{maxy[4]}{maxz[4]}, {ref[4]}, pad.  A wide node is a
+// two-level collapse of the reference LBVH node N whose entries are listed in the reference's
+// DFS order: [L if leaf][R if leaf] + expand(R) + expand(L), expand(X) = [XL if leaf][XR if
+// leaf][XR if internal][XL if internal].  Testing an entry's box directly instead of its
+// skipped binary ancestor's is exact (the entry box is inside the ancestor box: the slab
+// interval can only shrink), and leaves keep the exact re-test, so every pixel is identical to
+// the reference order; a ray needs about half the dependent node steps.
+template <int STACK>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void renderKernelW4(RenderParams P) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    const int tile = tileOf(P, blockIdx.x);
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int col = tx * 8 + (lane & 7);
+    const int lrow = ty * 8 + (lane >> 3);
+    const bool valid = col < P.width && lrow < P.nrows;
+    const size_t idx = valid ? (size_t)lrow * P.width + col : 0;
+    const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
+    if ((int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
+    const float fcol = (float)col;
+    const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
+    const DevScene& S = P.S;
+    uint32_t* my = stk + lane;
+    // Work counters are wave totals kept in scalar registers: each step adds the popcount of
+    // a ballot of the lanes that did the work (no per-lane counter VGPRs).
+    uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
+
+    Xorwow g{0, 0, 0, 0, 0, 0};
+    if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+    float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
+    float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
+    float closest = 0.0f;
+    int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
+    int nmask = -1;   // -1: `node` not visited yet; else its entries still to process (bit k = entry k)
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: leaf refs in DFS order
+    bool active = false;
+
+    // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
+    // captured variables address-taken and they end up in scratch memory.)
+#define PT_BEGIN_RAY()                                                                              \
+    do {                                                                                          \
+        depthLeft--;                                                                              \
+        closest = __builtin_inff();                                                               \
+        best = -1;                                                                                \
+        sp = 0;                                                                                   \
+        qn = 0;                                                                                   \
+        if (S.nprims <= 1) {                                                                      \
+            node = -1;                                                                            \
+            if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
+                const float t1 = primHitT(loadPrim(S, 0), __float_as_uint(S.prims[2].w) != 0, o, d, \
+                                          0.001f, closest);                                       \
+                if (t1 >= 0.0f) { closest = t1; best = 0; }                                       \
+            }                                                                                     \
+        } else {                                                                                  \
+            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
+            node = 0;                                                                             \
+            nmask = -1;                                                                           \
+        }                                                                                         \
+    } while (0)
+    // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
+#define PT_NEW_PATH()                                                                               \
+    do {                                                                                          \
+        const float u_ = (fcol + g.uniform()) * P.invW;                                           \
+        const float v_ = (frow + g.uniform()) * P.invH;                                           \
+        o = P.cam.pos;                                                                            \
+        d = sub(add(add(P.cam.ll, scale(u_, P.cam.hor)), scale(v_, P.cam.ver)), P.cam.pos);       \
+        att = f3(1.0f, 1.0f, 1.0f);                                                               \
+        depthLeft = P.max_depth;                                                                  \
+    } while (0)
+
+    bool started = false;
+    if (valid) {
+        if (P.max_depth <= 0) {
+            for (; sample < P.spp; sample++) { PT_NEW_PATH(); sum = add(sum, sky(d, att)); }
+        } else if (P.spp > 0) {
+            PT_NEW_PATH();
+            PT_BEGIN_RAY();
+            active = true;
+            started = true;
+        }
+    }
+    sRays += (uint32_t)__popcll(__ballot(started));
+    sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)P.spp : 0u);
+
+    for (;;) {
+        const bool wantNode = node >= 0 && qn < kLeafQ;
+        const bool wantLeaf = qn > 0;
+        const bool wantShade = active && node < 0 && qn == 0;
+        const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
+        if ((mN | mL | mS) == 0) break;
+        const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
+        int kind;   // 0 node, 1 leaf, 2 shade
+        if (nN == 0) kind = nL > 0 ? 1 : 2;
+        else if (nL >= P.leafBatch) kind = 1;
+        else if (nS >= P.shadeBatch) kind = 2;
+        else kind = 0;
+
+        if (kind == 0) {
+            // ------------------------------------------------------------------ NODE
+            sVisits += (uint32_t)nN;
+            if (wantNode) {
+                const float4* np = S.wnodes + 8 * (size_t)node;
+                int mask;
+                if (nmask < 0) {   // first visit: test the 4 entry boxes (SoA) against `closest`
+                    const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
+                    mask = (slab(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, 0.001f, closest) ? 1 : 0) |
+                           (slab(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, 0.001f, closest) ? 2 : 0) |
+                           (slab(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, 0.001f, closest) ? 4 : 0) |
+                           (slab(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, 0.001f, closest) ? 8 : 0);
+                } else {
+                    mask = nmask;   // resumed continuation: boxes were tested at the first visit
+                }
+                const float4 rf = np[6];
+                const uint32_t refs[4] = {__float_as_uint(rf.x), __float_as_uint(rf.y), __float_as_uint(rf.z),
+                                          __float_as_uint(rf.w)};
+                // Entries are stored in the reference's DFS order: queue leading leaves, descend into
+                // the first internal entry, push the rest as one continuation (node, remaining mask).
+                int next = -1;
+                bool stalled = false;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const bool take = next < 0 && !stalled && ((mask >> k) & 1);
+                    if (take) {
+                        const uint32_t ref = refs[k];
+                        if (ref & kLeafBit) {
+                            if (qn < kLeafQ) {
+                                q0 = qn == 0 ? ref : q0; q1 = qn == 1 ? ref : q1; q2 = qn == 2 ? ref : q2; q3 = qn == 3 ? ref : q3;
+                                qn++;
+                                mask &= ~(1 << k);
+                            } else {
+                                stalled = true;
+                            }
+                        } else {
+                            mask &= ~(1 << k);
+                            next = (int)ref;
+                        }
+                    }
+                }
+                if (next >= 0) {
+                    if (mask) {
+                        if (sp < STACK) { my[sp * kWave] = ((uint32_t)node << 4) | (uint32_t)mask; sp++; }
+                        else { atomicOr(S.err, 2u); }
+                    }
+                    node = next;
+                    nmask = -1;
+                } else if (mask) {   // leaf queue full: resume this node later
+                    nmask = mask;
+                } else if (sp > 0) {
+                    sp--;
+                    const uint32_t e = my[sp * kWave];
+                    node = (int)(e >> 4);
+                    nmask = (int)(e & 15u);
+                } else {
+                    node = -1;
+                }
+            }
+        } else if (kind == 1) {
+            // ------------------------------------------------------------------ LEAF
+            bool tested = false, sph = false;
+            if (wantLeaf) {
+                const uint32_t ref = q0;
+                q0 = q1; q1 = q2; q2 = q3;
+                qn--;
+                const uint32_t k = ref & kPrimMask;
+                sph = (ref & kSphereBit) != 0;
+                const Prim pr = loadPrim(S, k);
+                if (primBoxHit(pr, sph, o, inv, 0.001f, closest)) {
+                    tested = true;
+                    const float t = primHitT(pr, sph, o, d, 0.001f, closest);
+                    if (t >= 0.0f) { closest = t; best = (int)k; }
+                }
+            }
+            sTris += (uint32_t)__popcll(__ballot(tested && !sph));
+            sSph += (uint32_t)__popcll(__ballot(tested && sph));
+        } else {
+            // ------------------------------------------------------------------ SHADE
+            bool newRay = false, newSample = false;
+            if (wantShade) {
+                bool done = false;
+                float3 contrib = f3(0.0f, 0.0f, 0.0f);
+                if (best < 0) {
+                    contrib = sky(d, att);
+                    done = true;
+                } else {
+                    HitRec h = makeHit(S, best, closest, o, d);
+                    float3 na;
+                    if (!scatter(S, h, d, na, g)) {
+                        done = true;
+                    } else {
+                        att = mul(att, na);
+                        o = h.p;
+                        if (depthLeft == 0) { contrib = sky(d, att); done = true; }
+                    }
+                }
+                if (done) {
+                    sum = add(sum, contrib);
+                    if (++sample == P.spp) {
+                        active = false;
+                    } else {
+                        PT_NEW_PATH();
+                        PT_BEGIN_RAY();
+                        newRay = newSample = true;
+                    }
+                } else {
+                    PT_BEGIN_RAY();
+                    newRay = true;
+                }
+            }
+            sRays += (uint32_t)__popcll(__ballot(newRay));
+            sPaths += (uint32_t)__popcll(__ballot(newSample));
+        }
+    }
+    if (valid) {
+        float* outp = P.out + 3 * idx;   // main.cu:290-293
+        outp[0] = sqrtf(sum.x * P.invSpp);
+        outp[1] = sqrtf(sum.y * P.invSpp);
+        outp[2] = sqrtf(sum.z * P.invSpp);
+        P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+    }
+    const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
+    if (P.waveTimes && lane == 0) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        P.waveTimes[3 * (size_t)blockIdx.x + 0] = tStart;
+        P.waveTimes[3 * (size_t)blockIdx.x + 1] = tEnd;
+        P.waveTimes[3 * (size_t)blockIdx.x + 2] = (unsigned long long)tile | ((unsigned long long)(xcc & 0xf) << 32);
+    }
+    if (lane == 0) {
+        atomicAdd(P.counters + 0, (unsigned long long)sRays);
+        atomicAdd(P.counters + 1, (unsigned long long)sVisits);
+        atomicAdd(P.counters + 2, (unsigned long long)sTris);
+        atomicAdd(P.counters + 3, (unsigned long long)sSph);
+        atomicAdd(P.counters + 4, (unsigned long long)sPaths);
+    }
+}
+#undef PT_BEGIN_RAY
+#undef PT_NEW_PATH
+
 template <int STACK>
 __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* rays, int64_t n, float tmin,
                                                      float tmax, pt_hit* hits, unsigned long long* counters) {
@@ -920,6 +1163,9 @@ struct pt_scene {
     std::vector<uint64_t> keys;             // sorted Morton keys of the current BVH
     std::vector<int32_t> iparent, lparent;  // host copies for download
     std::vector<float> leafBoxes;           // 6 floats per leaf slot
+    DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelW4)
+    int wideDepth = 0;
+    int64_t wideNodes = 0;
     int depth = 0;
     bool built = false;
     size_t deviceBytes = 0;
@@ -938,6 +1184,79 @@ struct pt_film {
 };
 
 namespace {
+// Collapse the binary LBVH (device records downloaded into `bin`) into 4-wide nodes whose
+// entries follow the reference's DFS order (see renderKernelW4).
+int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
+    auto refOf = [&](int n, int slot) {
+        float f = slot == 0 ? bin[4 * (size_t)n + 3].x : bin[4 * (size_t)n + 3].y;
+        uint32_t r;
+        std::memcpy(&r, &f, 4);
+        return r;
+    };
+    auto boxOf = [&](int n, int slot, float b[6]) {
+        const float* f = reinterpret_cast<const float*>(&bin[4 * (size_t)n]) + 6 * slot;
+        for (int i = 0; i < 6; i++) b[i] = f[i];
+    };
+    struct Entry { uint32_t ref; bool internal; float box[6]; };
+    std::vector<float> out;   // 32 floats per wide node
+    std::vector<std::pair<int, int>> work{{0, 0}};   // (binary node, wide index)
+    std::vector<int> depth{1};
+    out.resize(32);
+    int maxDepth = 1;
+    for (size_t qi = 0; qi < work.size(); qi++) {
+        const int n = work[qi].first, w = work[qi].second;
+        std::vector<Entry> e;
+        auto add = [&](int parent, int slot) {
+            Entry x;
+            x.ref = refOf(parent, slot);
+            x.internal = !(x.ref & kLeafBit);
+            boxOf(parent, slot, x.box);
+            e.push_back(x);
+        };
+        auto expand = [&](int x) {   // [XL if leaf][XR if leaf][XR if internal][XL if internal]
+            const uint32_t xl = refOf(x, 0), xr = refOf(x, 1);
+            if (xl & kLeafBit) add(x, 0);
+            if (xr & kLeafBit) add(x, 1);
+            if (!(xr & kLeafBit)) add(x, 1);
+            if (!(xl & kLeafBit)) add(x, 0);
+        };
+        const uint32_t l = refOf(n, 0), r = refOf(n, 1);
+        if (l & kLeafBit) add(n, 0);
+        if (r & kLeafBit) add(n, 1);
+        if (!(r & kLeafBit)) expand((int)r);
+        if (!(l & kLeafBit)) expand((int)l);
+        float* W = &out[32 * (size_t)w];
+        for (int k = 0; k < 4; k++) {
+            const float inf = std::numeric_limits<float>::infinity();
+            float b[6] = {inf, inf, inf, -inf, -inf, -inf};
+            uint32_t ref = 0;
+            if (k < (int)e.size()) {
+                for (int i = 0; i < 6; i++) b[i] = e[k].box[i];
+                ref = e[k].ref;
+                if (e[k].internal) {
+                    const int wi = (int)(out.size() / 32);
+                    out.resize(out.size() + 32);
+                    W = &out[32 * (size_t)w];
+                    work.push_back({(int)e[k].ref, wi});
+                    depth.push_back(depth[qi] + 1);
+                    maxDepth = std::max(maxDepth, depth[qi] + 1);
+                    ref = (uint32_t)wi;
+                }
+            }
+            for (int a = 0; a < 6; a++) W[4 * a + k] = b[a];   // SoA planes
+            std::memcpy(&W[24 + k], &ref, 4);
+        }
+        for (int k = 28; k < 32; k++) W[k] = 0.0f;
+    }
+    if (out.size() / 32 >= (1u << 27)) return fail(PT_ERR_STATE, "too many wide nodes");
+    int rc;
+    if ((rc = devAlloc(s->wide, out.size() * 4))) return rc;
+    HIP_TRY(hipMemcpy(s->wide.p, out.data(), out.size() * 4, hipMemcpyHostToDevice));
+    s->wideDepth = maxDepth;
+    s->wideNodes = (int64_t)(out.size() / 32);
+    return PT_OK;
+}
+
 int setDevice(int dev) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
@@ -949,7 +1268,8 @@ int setDevice(int dev) {
 
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
-    if (P.leafBatch > 0) renderKernelWF<S><<<P.ntiles, kWave, 0, st>>>(P);
+    if (P.kernel == PT_KERNEL_WIDE) renderKernelW4<S><<<P.ntiles, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
 }
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
@@ -997,6 +1317,7 @@ DevScene devScene(const pt_scene* s) {
     S.prims = s->prims.as<float4>();
     S.normals = s->normals.as<float4>();
     S.mats = s->mats.as<float4>();
+    S.wnodes = s->wide.as<float4>();
     S.err = reinterpret_cast<unsigned int*>(s->counters.as<unsigned long long>() + 7);
     S.nprims = (int)s->nobj;
     return S;
@@ -1158,6 +1479,7 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
             }
         }
         s->depth = maxd;
+        if ((rc = buildWide4(s, tmp))) return rc;
     }
     if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
     s->deviceBytes = (size_t)ni * 64 + (size_t)n * 64 + (size_t)s->nmat * 32;
@@ -1379,14 +1701,17 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     int kernel = opts ? opts->kernel : PT_KERNEL_DEFAULT;
     if (kernel == PT_KERNEL_DEFAULT) {
         const char* k = std::getenv("PT_RENDER_KERNEL");
-        kernel = (k && std::string(k) == "simple") ? PT_KERNEL_SIMPLE : PT_KERNEL_WAVEFRONT;
+        const std::string ks = k ? k : "";
+        kernel = ks == "simple" ? PT_KERNEL_SIMPLE : (ks == "wavefront" ? PT_KERNEL_WAVEFRONT : PT_KERNEL_WIDE);
     }
-    if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT)
+    if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
         return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
+    if (kernel == PT_KERNEL_WIDE && s->nobj > 1 && !s->wide.p) return fail(PT_ERR_STATE, "wide BVH missing");
+    P.kernel = kernel;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64) : envInt("PT_LEAF_BATCH", 8);
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64) : envInt("PT_SHADE_BATCH", 16);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
-    const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
+    const int stack = s->nobj > 1 ? stackFor(kernel == PT_KERNEL_WIDE ? s->wideDepth : s->depth) : 16;
     const size_t ntl = (size_t)std::max(1, P.ntiles);
     if (!f->tileCost.p) {
         if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4))) return rc;
@@ -1399,7 +1724,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
-    if (timesPath && *timesPath && kernel == PT_KERNEL_WAVEFRONT) {
+    if (timesPath && *timesPath && kernel != PT_KERNEL_SIMPLE) {
         if ((rc = devAlloc(dtimes, (size_t)std::max(1, P.ntiles) * 24))) return rc;
         HIP_TRY(hipMemsetAsync(dtimes.p, 0, (size_t)std::max(1, P.ntiles) * 24, st));
         P.waveTimes = dtimes.as<unsigned long long>();

@@ -54,7 +54,7 @@ class RenderOpts(C.Structure):
     _fields_ = [("kernel", C.c_int32), ("leaf_batch", C.c_int32), ("shade_batch", C.c_int32), ("reserved", C.c_int32)]
 
 
-KERNEL_DEFAULT, KERNEL_SIMPLE, KERNEL_WAVEFRONT = 0, 1, 2
+KERNEL_DEFAULT, KERNEL_SIMPLE, KERNEL_WAVEFRONT, KERNEL_WIDE = 0, 1, 2, 3
 
 
 class SceneDesc(C.Structure):

@@ -125,8 +125,8 @@ def render_both(pt, orc, gpu, p, w, h, spp, depth, seed=1, parts=1, part=0, stri
     return rgb, st, f.get_rng(), ref, rst, states, f
 
 
-KERNELS = [("wavefront", "16", "24"), ("simple", "16", "24"), ("wavefront", "1", "1"), ("wavefront", "64", "64"),
-           ("wavefront", "5", "50")]
+KERNELS = [("wide", "8", "16"), ("wavefront", "8", "16"), ("simple", "16", "24"), ("wide", "1", "1"),
+           ("wide", "64", "64"), ("wavefront", "5", "50")]
 
 
 @pytest.fixture(params=KERNELS, ids=lambda k: f"{k[0]}-L{k[1]}-S{k[2]}")
@@ -156,8 +156,8 @@ def test_render_bit_exact(pt, orc, gpu, kernel, name, w, h, spp, depth):
     assert st.tri_tests == rst.tri_tests and st.sphere_tests == rst.sphere_tests
     if kernel[0] == "simple":
         assert st.node_visits == rst.node_visits
-    else:
-        assert st.node_visits >= rst.node_visits
+    elif kernel[0] == "wavefront":
+        assert st.node_visits >= rst.node_visits   # speculative traversal: a few extra binary nodes
 
 
 @pytest.mark.parametrize("w,h,stripe", [(37, 19, 3), (50, 30, 8), (8, 8, 1)])
@@ -293,6 +293,10 @@ def test_film_reset_and_explicit_kernels(pt, gpu):
     b, sb = pt.render(s, f, p.camera, 3, 50, kernel=pt.KERNEL_WAVEFRONT, leaf_batch=9, shade_batch=33)
     np.testing.assert_array_equal(bits(a), bits(b))
     assert sa.rays == sb.rays and sa.tri_tests == sb.tri_tests
+    f.reset()
+    c, sc = pt.render(s, f, p.camera, 3, 50, kernel=pt.KERNEL_WIDE, leaf_batch=5, shade_batch=20)
+    np.testing.assert_array_equal(bits(a), bits(c))
+    assert sa.rays == sc.rays and sa.tri_tests == sc.tri_tests
     with pytest.raises(pt.PtError):
         pt.render(s, f, p.camera, 1, 5, kernel=7)
 

@@ -13,8 +13,8 @@ import ptamd  # noqa: E402
 
 name = {"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[sys.argv[1] if len(sys.argv) > 1 else "c3"]
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 128
-settings = [("simple", 16, 24)] + [("wavefront", l, s) for l, s in
-            [(8, 16), (16, 24), (24, 32), (32, 48), (12, 40), (16, 48), (24, 56), (8, 32), (40, 40)]]
+settings = [("simple", 16, 24), ("wavefront", 8, 16)] + [("wide", l, s) for l, s in
+            [(4, 12), (6, 16), (8, 16), (8, 24), (12, 16), (12, 24), (16, 24), (16, 32)]]
 if len(sys.argv) > 3:
     settings = [tuple(x.split(":")[:1]) + tuple(int(v) for v in x.split(":")[1:]) for x in sys.argv[3].split(",")]
 p = ptamd.Preset(name)
