@@ -717,7 +717,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
     int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
-    int nmask = -1;   // -1: `node` not visited yet; else its entries still to process (bit k = entry k)
+    // node >= 0: wide node to visit; -2: the stack top must be popped (a leaf waiting for queue
+    // space); -1: traversal of the current ray complete
     uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: leaf refs in DFS order
     bool active = false;
 
@@ -740,7 +741,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         } else {                                                                                  \
             inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
             node = 0;                                                                             \
-            nmask = -1;                                                                           \
         }                                                                                         \
     } while (0)
     // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
@@ -769,9 +769,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)P.spp : 0u);
 
     for (;;) {
-        const bool wantNode = node >= 0 && qn < kLeafQ;
+        const bool wantNode = node >= 0 || (node == -2 && qn < kLeafQ);
         const bool wantLeaf = qn > 0;
-        const bool wantShade = active && node < 0 && qn == 0;
+        const bool wantShade = active && node == -1 && qn == 0;
         const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
@@ -785,59 +785,77 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
             // ------------------------------------------------------------------ NODE
             sVisits += (uint32_t)nN;
             if (wantNode) {
-                const float4* np = S.wnodes + 8 * (size_t)node;
-                int mask;
-                if (nmask < 0) {   // first visit: test the 4 entry boxes (SoA) against `closest`
+                bool needPop = node == -2;
+                if (node >= 0) {
+                    const float4* np = S.wnodes + 8 * (size_t)node;
                     const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
-                    mask = (slab(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, 0.001f, closest) ? 1 : 0) |
-                           (slab(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, 0.001f, closest) ? 2 : 0) |
-                           (slab(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, 0.001f, closest) ? 4 : 0) |
-                           (slab(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, 0.001f, closest) ? 8 : 0);
-                } else {
-                    mask = nmask;   // resumed continuation: boxes were tested at the first visit
-                }
-                const float4 rf = np[6];
-                const uint32_t refs[4] = {__float_as_uint(rf.x), __float_as_uint(rf.y), __float_as_uint(rf.z),
-                                          __float_as_uint(rf.w)};
-                // Entries are stored in the reference's DFS order: queue leading leaves, descend into
-                // the first internal entry, push the rest as one continuation (node, remaining mask).
-                int next = -1;
-                bool stalled = false;
+                    const float4 rf = np[6];
+                    int mask = (slab(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, 0.001f, closest) ? 1 : 0) |
+                               (slab(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, 0.001f, closest) ? 2 : 0) |
+                               (slab(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, 0.001f, closest) ? 4 : 0) |
+                               (slab(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, 0.001f, closest) ? 8 : 0);
+                    const uint32_t refs[4] = {__float_as_uint(rf.x), __float_as_uint(rf.y), __float_as_uint(rf.z),
+                                              __float_as_uint(rf.w)};
+                    // Entries are in the reference's DFS order.  Leading hit leaves go straight to
+                    // the leaf queue, the first hit internal entry is visited next, and the hit
+                    // entries after it are pushed individually in reverse order.
+                    int next = -1;
+                    bool full = false;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const bool take = next < 0 && !stalled && ((mask >> k) & 1);
-                    if (take) {
-                        const uint32_t ref = refs[k];
-                        if (ref & kLeafBit) {
-                            if (qn < kLeafQ) {
-                                q0 = qn == 0 ? ref : q0; q1 = qn == 1 ? ref : q1; q2 = qn == 2 ? ref : q2; q3 = qn == 3 ? ref : q3;
-                                qn++;
-                                mask &= ~(1 << k);
+                    for (int e = 0; e < 4; e++) {
+                        if (next < 0 && !full && ((mask >> e) & 1)) {
+                            const uint32_t ref = refs[e];
+                            if (ref & kLeafBit) {
+                                if (qn < kLeafQ) {
+                                    q0 = qn == 0 ? ref : q0; q1 = qn == 1 ? ref : q1; q2 = qn == 2 ? ref : q2; q3 = qn == 3 ? ref : q3;
+                                    qn++;
+                                    mask &= ~(1 << e);
+                                } else {
+                                    full = true;
+                                }
                             } else {
-                                stalled = true;
+                                next = (int)ref;
+                                mask &= ~(1 << e);
                             }
-                        } else {
-                            mask &= ~(1 << k);
-                            next = (int)ref;
                         }
                     }
-                }
-                if (next >= 0) {
-                    if (mask) {
-                        if (sp < STACK) { my[sp * kWave] = ((uint32_t)node << 4) | (uint32_t)mask; sp++; }
-                        else { atomicOr(S.err, 2u); }
+#pragma unroll
+                    for (int e = 3; e >= 0; e--) {
+                        if ((mask >> e) & 1) {
+                            if (sp < STACK) { my[sp * kWave] = refs[e]; sp++; }
+                            else { atomicOr(S.err, 2u); }
+                        }
                     }
-                    node = next;
-                    nmask = -1;
-                } else if (mask) {   // leaf queue full: resume this node later
-                    nmask = mask;
-                } else if (sp > 0) {
-                    sp--;
-                    const uint32_t e = my[sp * kWave];
-                    node = (int)(e >> 4);
-                    nmask = (int)(e & 15u);
-                } else {
+                    if (next >= 0) node = next;
+                    else if (full) node = -2;
+                    else needPop = true;
+                }
+                if (needPop) {   // pop queued leaves until an internal node (bounded)
                     node = -1;
+                    bool decided = false;
+#pragma unroll
+                    for (int it = 0; it < 4; it++) {
+                        if (!decided) {
+                            if (sp == 0) {
+                                decided = true;
+                            } else {
+                                const uint32_t e = my[(sp - 1) * kWave];
+                                if (!(e & kLeafBit)) {
+                                    node = (int)e;
+                                    sp--;
+                                    decided = true;
+                                } else if (qn < kLeafQ) {
+                                    q0 = qn == 0 ? e : q0; q1 = qn == 1 ? e : q1; q2 = qn == 2 ? e : q2; q3 = qn == 3 ? e : q3;
+                                    qn++;
+                                    sp--;
+                                } else {
+                                    node = -2;
+                                    decided = true;
+                                }
+                            }
+                        }
+                    }
+                    if (!decided) node = sp > 0 ? -2 : -1;
                 }
             }
         } else if (kind == 1) {
@@ -1201,6 +1219,8 @@ int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
     std::vector<float> out;   // 32 floats per wide node
     std::vector<std::pair<int, int>> work{{0, 0}};   // (binary node, wide index)
     std::vector<int> depth{1};
+    std::vector<int> nent{0};                           // entries per wide node
+    std::vector<std::vector<int>> kids(1);              // internal children per wide node
     out.resize(32);
     int maxDepth = 1;
     for (size_t qi = 0; qi < work.size(); qi++) {
@@ -1239,6 +1259,9 @@ int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
                     W = &out[32 * (size_t)w];
                     work.push_back({(int)e[k].ref, wi});
                     depth.push_back(depth[qi] + 1);
+                    nent.push_back(0);
+                    kids.emplace_back();
+                    kids[w].push_back(wi);
                     maxDepth = std::max(maxDepth, depth[qi] + 1);
                     ref = (uint32_t)wi;
                 }
@@ -1247,12 +1270,22 @@ int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
             std::memcpy(&W[24 + k], &ref, 4);
         }
         for (int k = 28; k < 32; k++) W[k] = 0.0f;
+        nent[w] = (int)e.size();
+    }
+    // Worst-case stack use of renderKernelW4 (every entry hit): a visit pushes at most
+    // entries-1 items, then one subtree below it is active.  Children have larger indices.
+    std::vector<int> need(nent.size(), 0);
+    for (size_t w = nent.size(); w-- > 0;) {
+        int sub = 0;
+        for (int c : kids[w]) sub = std::max(sub, need[c]);
+        need[w] = std::max(0, nent[w] - 1) + sub;
     }
     if (out.size() / 32 >= (1u << 27)) return fail(PT_ERR_STATE, "too many wide nodes");
     int rc;
     if ((rc = devAlloc(s->wide, out.size() * 4))) return rc;
     HIP_TRY(hipMemcpy(s->wide.p, out.data(), out.size() * 4, hipMemcpyHostToDevice));
-    s->wideDepth = maxDepth;
+    s->wideDepth = need[0] + 1;   // stack entries needed (template choice); depth kept for info
+    (void)maxDepth;
     s->wideNodes = (int64_t)(out.size() / 32);
     return PT_OK;
 }
