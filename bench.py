@@ -170,7 +170,7 @@ def main() -> None:
                        "rng": "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "renderKernelW4", "kernel_ms_per_launch": kms / args.steps,
+                         "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
                          "algo_bytes_per_launch": kbytes / args.steps,
                          "algo_bytes_source": "reference-order traversal counts of the same frame "
                                               "(ray-synchronous kernel, warmup step 1)",

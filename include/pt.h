@@ -142,8 +142,8 @@ int pt_film_set_rng(pt_film* film, const uint32_t* states);
  * else a host pointer.  The film's RNG streams advance, as the reference's devStates do. */
 int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
               float* out_rgb, int out_on_device, void* stream, pt_stats* stats);
-/* Render options.  kernel: PT_KERNEL_DEFAULT (= PT_KERNEL_WIDE unless the PT_RENDER_KERNEL
- * environment variable says "simple" or "wavefront"), PT_KERNEL_SIMPLE (ray-synchronous, the
+/* Render options.  kernel: PT_KERNEL_DEFAULT (= PT_KERNEL_WAVEFRONT unless the PT_RENDER_KERNEL
+ * environment variable says "simple" or "wide"), PT_KERNEL_SIMPLE (ray-synchronous, the
  * reference's loop structure, binary LBVH), PT_KERNEL_WAVEFRONT (per-lane state machine, steps
  * chosen by wave ballots, binary LBVH) or PT_KERNEL_WIDE (the same on the 4-wide collapse of
  * the LBVH).  All give bit-identical images.  leaf_batch / shade_batch: wavefront thresholds
