@@ -76,6 +76,10 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--leaf-batch", type=int, default=0, help="wavefront LEAF threshold (0 = library default)")
     ap.add_argument("--shade-batch", type=int, default=0, help="wavefront SHADE threshold (0 = library default)")
+    ap.add_argument("--rng", default="compat", choices=["compat", "sample"],
+                    help="compat: the reference's per-pixel cuRAND-XORWOW streams (bit-exact parity mode); "
+                         "sample: Philox per pixel-sample, (tile, sample-chunk) work units")
+    ap.add_argument("--chunk", type=int, default=0, help="sample mode: samples per work unit (0 = library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,12 +103,17 @@ def main() -> None:
     gathered = torch.empty((world * max_rows * w * 3,), dtype=torch.float32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
+    sample = args.rng == "sample"
+
     def frame(kernel=ptamd.KERNEL_DEFAULT):
         # every step renders the SAME frame: streams back to curand_init(seed, pixel, 0)
-        film.reset(stream.cuda_stream)
+        # (sample mode is stateless: a pure function of seed, pixel and sample)
+        if not sample:
+            film.reset(stream.cuda_stream)
         _, st = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
                              stream=stream.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
-                             shade_batch=args.shade_batch)
+                             shade_batch=args.shade_batch, rng=ptamd.RNG_SAMPLE if sample else ptamd.RNG_COMPAT,
+                             chunk=args.chunk)
         if world > 1:
             dist.all_gather_into_tensor(gathered, local_buf)
         return st
@@ -113,7 +122,9 @@ def main() -> None:
     # order exactly: its counters give the frame's ALGORITHMIC bytes (the wavefront kernel may
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
-    ref_st = frame(ptamd.KERNEL_SIMPLE)
+    # Sample mode runs on the wavefront kernel only: its own counters are used (they include the
+    # speculative node visits, +0.27% on C3 in compat mode, so `achieved` is overstated by that).
+    ref_st = frame() if sample else frame(ptamd.KERNEL_SIMPLE)
     for _ in range(max(0, args.warmup - 1)):
         frame()
     if world > 1:
@@ -167,13 +178,17 @@ def main() -> None:
             "config": {"workload": workload, "width": w, "height": h, "spp": spp, "max_depth": depth,
                        "stripe_rows": STRIPE, "parallelism": f"rows{world}",
                        "rays_per_frame": total_rays / args.steps,
-                       "rng": "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
+                       "rng": ("Philox4x32-10 per pixel-sample (sample mode), chunk "
+                               f"{args.chunk or 64}") if sample else
+                              "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
                          "algo_bytes_per_launch": kbytes / args.steps,
-                         "algo_bytes_source": "reference-order traversal counts of the same frame "
-                                              "(ray-synchronous kernel, warmup step 1)",
+                         "algo_bytes_source": ("wavefront-kernel counters of the same frame (incl. speculative "
+                                               "node visits)") if sample else
+                                              ("reference-order traversal counts of the same frame "
+                                               "(ray-synchronous kernel, warmup step 1)"),
                          "node_visits_reference": ref_st.node_visits,
                          "node_visits_wavefront": spec_visits / args.steps},
         }

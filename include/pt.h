@@ -142,14 +142,28 @@ int pt_film_set_rng(pt_film* film, const uint32_t* states);
  * else a host pointer.  The film's RNG streams advance, as the reference's devStates do. */
 int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
               float* out_rgb, int out_on_device, void* stream, pt_stats* stats);
-/* Render options.  kernel: PT_KERNEL_DEFAULT (= PT_KERNEL_WAVEFRONT unless the PT_RENDER_KERNEL
- * environment variable says "simple" or "wide"), PT_KERNEL_SIMPLE (ray-synchronous, the
- * reference's loop structure, binary LBVH), PT_KERNEL_WAVEFRONT (per-lane state machine, steps
- * chosen by wave ballots, binary LBVH) or PT_KERNEL_WIDE (the same on the 4-wide collapse of
- * the LBVH).  All give bit-identical images.  leaf_batch / shade_batch: wavefront thresholds
- * in lanes (0 = default).  reserved = 1 disables the longest-tile-first launch order. */
+/* Render options.
+ * kernel: PT_KERNEL_DEFAULT (= PT_KERNEL_WAVEFRONT unless the PT_RENDER_KERNEL environment
+ *   variable says "simple" or "wide"), PT_KERNEL_SIMPLE (ray-synchronous, the reference's loop
+ *   structure, binary LBVH), PT_KERNEL_WAVEFRONT (per-lane state machine, steps chosen by wave
+ *   ballots, binary LBVH) or PT_KERNEL_WIDE (the same on the 4-wide collapse of the LBVH).
+ *   All kernels give bit-identical images for a given rng mode.
+ * rng: PT_RNG_COMPAT (default): the reference's semantics -- one cuRAND-XORWOW stream per
+ *   pixel, curand_init(seed, pixel, 0), samples consumed in order and kept across calls like
+ *   the reference's devStates; a pixel's samples are inherently sequential.
+ *   PT_RNG_SAMPLE: one counter-based Philox4x32-10 stream per pixel-sample (key = film seed,
+ *   counter = {draw/4, sample, pixel}); work units are (8x8 tile, chunk of `chunk` samples)
+ *   (0 = 64), chunk sums are added in chunk order.  Deterministic, statistically identical to
+ *   the reference, not its random numbers; does not advance the film's XORWOW streams.
+ * leaf_batch / shade_batch: wavefront thresholds in lanes (0 = default).
+ * flags: PT_RENDER_IDENTITY_ORDER disables the longest-tile-first launch order. */
 enum { PT_KERNEL_DEFAULT = 0, PT_KERNEL_SIMPLE = 1, PT_KERNEL_WAVEFRONT = 2, PT_KERNEL_WIDE = 3 };
-typedef struct { int32_t kernel, leaf_batch, shade_batch, reserved; } pt_render_opts;
+enum { PT_RNG_COMPAT = 0, PT_RNG_SAMPLE = 1 };
+#define PT_RENDER_IDENTITY_ORDER 1
+typedef struct {
+    int32_t kernel, leaf_batch, shade_batch, flags;
+    int32_t rng, chunk, reserved0, reserved1;
+} pt_render_opts;
 int pt_render_ex(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
                  float* out_rgb, int out_on_device, void* stream, const pt_render_opts* opts,
                  pt_stats* stats);

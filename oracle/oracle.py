@@ -55,6 +55,9 @@ for name, res, args in [
     ("orc_scatter_tape", C.c_int, [_P, _P, _P, _P, C.c_int, C.POINTER(C.c_int), _P, _P]),
     ("orc_render2", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
                               C.c_int, _P, _P, C.POINTER(Stats), C.c_int, _P]),
+    ("orc_render_sample", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
+                                    C.c_int, C.c_uint64, C.c_int, _P, C.POINTER(Stats), C.c_int]),
+    ("orc_philox_word", C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]),
     ("orc_render", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
                              C.c_int, _P, _P, C.POINTER(Stats), C.c_int]),
 ]:
@@ -161,6 +164,21 @@ def render(objects, materials, nodes, camera: np.ndarray, width: int, height: in
     return out, st
 
 
+def render_sample(objects, materials, nodes, camera, width, height, rows, spp, max_depth, seed, chunk=64,
+                  nthreads=1):
+    """Sample mode (Philox per pixel-sample, chunked sums): (rgb float32 (npix, 3), Stats)."""
+    objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+    materials = np.ascontiguousarray(materials, MATERIAL_DTYPE)
+    rows = np.ascontiguousarray(rows, np.int32)
+    camera = np.ascontiguousarray(camera, np.float32)
+    out = np.zeros((len(rows) * width, 3), np.float32)
+    st = Stats()
+    lib.orc_render_sample(_ptr(objects), len(objects), _ptr(materials), len(materials), _ptr(nodes), _ptr(camera),
+                          width, height, _ptr(rows), len(rows), spp, max_depth, seed, chunk, _ptr(out), C.byref(st),
+                          nthreads)
+    return out, st
+
+
 def render_pixel_rays(objects, materials, nodes, camera, width, height, rows, spp, max_depth, states, nthreads=1):
     """orc_render + per-pixel ray counts: (rgb, rays uint32 (npix,), Stats)."""
     objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
@@ -189,3 +207,8 @@ def film_states(seed: int, width: int, rows) -> np.ndarray:
         out[i * width:(j + 1) * width] = xorwow_init_range(seed, int(rows[i]) * width, (j - i + 1) * width)
         i = j + 1
     return out
+
+
+def philox_word(seed: int, sample: int, pixel: int, draw: int) -> int:
+    """Sample-mode generator: uniform draw `draw` of pixel-sample (pixel, sample)."""
+    return int(lib.orc_philox_word(seed, sample, pixel, draw))

@@ -273,6 +273,33 @@ struct XorwowRng {
     uint32_t* s;
     float operator()() { return curandUniform(s); }
 };
+
+// Philox4x32-10 (Salmon et al. 2011; the generator cuRAND offers as curandStatePhilox4_32_10).
+// Sample mode stream of pixel p, sample s: key = seed, counter = {block, s, p_lo, p_hi}; draw i
+// is word (i % 4) of block (i / 4).  Uniform mapping as curand_uniform: u * 2^-32 + 2^-33.
+inline void philoxBlock(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t out[4]) {
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+struct PhiloxRng {
+    uint32_t k0, k1, sample, p0, p1, draw = 0;
+    uint32_t buf[4] = {0, 0, 0, 0};
+    float operator()() {
+        if ((draw & 3u) == 0) philoxBlock(draw >> 2, sample, p0, p1, k0, k1, buf);
+        const uint32_t x = buf[draw & 3u];
+        draw++;
+        const float k = 2.3283064e-10f;
+        return (float)x * k + (k / 2.0f);
+    }
+};
 struct TapeRng {
     const float* tape; int len; int pos;
     float operator()() { return pos < len ? tape[pos++] : (pos++, 0.5f); }
@@ -606,6 +633,39 @@ int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, i
                        stats, nthreads, nullptr);
 }
 
+}  // extern "C"
+
+namespace {
+// One camera sample of pixel (col, row): main.cu:284-288 (rng draws u, v, then the bounces).
+template <class R>
+V3 tracePath(const orc_object* objs, int64_t nobj, const orc_material* mats, const orc_node* nodes, const orc_camera* cam,
+             int col, int row, float invW, float invH, int max_depth, R& rng, orc_stats& local) {
+    const V3 pos = load3(cam->origin), ll = load3(cam->lower_left);
+    const V3 hor = load3(cam->horizontal), ver = load3(cam->vertical);
+    float u = ((float)col + rng()) * invW;
+    float v = ((float)row + rng()) * invH;
+    Ray cur{pos, ((ll + u * hor) + v * ver) - pos};
+    local.paths++;
+    V3 att{1, 1, 1};
+    int depth = max_depth;
+    while (depth-- > 0) {
+        Hit rec;
+        local.rays++;
+        if (!hitBvh(objs, nobj, nodes, cur, 0.001f, std::numeric_limits<float>::infinity(), rec, &local)) break;
+        V3 na;
+        Ray sc;
+        if (!scatter(mats[rec.mat], cur, rec, na, sc, rng)) return {0, 0, 0};
+        att = att * na;
+        cur = sc;
+    }
+    V3 ud = normalize(cur.d);
+    float t = 0.5f * (ud.y + 1.0f);
+    return ((1.0f - t) * v3(1.0f, 1.0f, 1.0f) + t * v3(0.5f, 0.7f, 1.0f)) * att;
+}
+}  // namespace
+
+extern "C" {
+
 int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
                 const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
                 uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays) {
@@ -681,6 +741,64 @@ int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, 
     worker();
     for (auto& t : th) t.join();
     return 0;
+}
+
+int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
+                      const orc_node* nodes, const orc_camera* cam, int width, int height, const int32_t* rows,
+                      int nrows, int spp, int max_depth, uint64_t seed, int chunk, float* out_rgb, orc_stats* stats,
+                      int nthreads) {
+    (void)nmat;
+    if (nthreads < 1) nthreads = 1;
+    if (chunk < 1) chunk = 1;
+    const float invW = 1.0f / (float)width, invH = 1.0f / (float)height, invSpp = 1.0f / (float)spp;
+    std::atomic<int> next{0};
+    std::mutex mu;
+    auto worker = [&]() {
+        orc_stats local{};
+        for (;;) {
+            int ri = next.fetch_add(1);
+            if (ri >= nrows) break;
+            const int row = rows[ri];
+            for (int col = 0; col < width; col++) {
+                const uint64_t pixel = (uint64_t)row * (uint64_t)width + (uint64_t)col;
+                V3 total{0, 0, 0};
+                for (int c0 = 0; c0 < spp; c0 += chunk) {   // chunks summed in order
+                    V3 part{0, 0, 0};
+                    for (int s = c0; s < std::min(spp, c0 + chunk); s++) {
+                        PhiloxRng rng{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)s, (uint32_t)pixel,
+                                      (uint32_t)(pixel >> 32)};
+                        part = part + tracePath(objs, nobj, mats, nodes, cam, col, row, invW, invH, max_depth, rng, local);
+                    }
+                    total = total + part;
+                }
+                const int64_t k = (int64_t)ri * width + col;
+                out_rgb[3 * k + 0] = std::sqrt(total.x * invSpp);
+                out_rgb[3 * k + 1] = std::sqrt(total.y * invSpp);
+                out_rgb[3 * k + 2] = std::sqrt(total.z * invSpp);
+            }
+        }
+        if (stats) {
+            std::lock_guard<std::mutex> g(mu);
+            stats->rays += local.rays;
+            stats->node_visits += local.node_visits;
+            stats->box_tests += local.box_tests;
+            stats->tri_tests += local.tri_tests;
+            stats->sphere_tests += local.sphere_tests;
+            stats->paths += local.paths;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; t++) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+    return 0;
+}
+
+uint32_t orc_philox_word(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t draw) {
+    PhiloxRng rng{(uint32_t)seed, (uint32_t)(seed >> 32), sample, (uint32_t)pixel, (uint32_t)(pixel >> 32)};
+    uint32_t out[4];
+    philoxBlock(draw >> 2, sample, (uint32_t)pixel, (uint32_t)(pixel >> 32), rng.k0, rng.k1, out);
+    return out[draw & 3u];
 }
 
 }  // extern "C"

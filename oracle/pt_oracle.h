@@ -77,6 +77,15 @@ int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, 
                 const int32_t* rows, int nrows, int spp, int max_depth,
                 uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays);
 
+/* Sample mode: one Philox4x32-10 stream per pixel-sample (key = seed, counter = {draw/4,
+ * sample, pixel_lo, pixel_hi}); samples summed per chunk of `chunk` samples, chunk sums
+ * summed in order, sqrt(total / spp).  Same rows/out layout as orc_render. */
+int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
+                      const orc_node* nodes, const orc_camera* cam, int width, int height,
+                      const int32_t* rows, int nrows, int spp, int max_depth, uint64_t seed, int chunk,
+                      float* out_rgb, orc_stats* stats, int nthreads);
+uint32_t orc_philox_word(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t draw);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <type_traits>
 #include <memory>
 #include <string>
 #include <vector>
@@ -97,6 +98,34 @@ struct Xorwow {
     }
     // curand_uniform: x * 2^-32 + 2^-33 in (0, 1]
     __device__ __forceinline__ float uniform() { return (float)next() * 0x1p-32f + 0x1p-33f; }
+};
+
+// Philox4x32-10 (Salmon et al. 2011), the counter-based generator of sample mode: the stream
+// of (pixel p, sample s) is key = seed, counter = {draw / 4, s, p_lo, p_hi}; draw i is word
+// i % 4 of block i / 4; uniform mapping as curand_uniform.  Any sample can start anywhere.
+struct Philox {
+    uint32_t k0, k1, sample, pixel, draw;
+    uint32_t b0, b1, b2, b3;
+    __device__ __forceinline__ void block() {
+        uint32_t c0 = draw >> 2, c1 = sample, c2 = pixel, c3 = 0u, x0 = k0, x1 = k1;
+#pragma unroll
+        for (int r = 0; r < 10; r++) {
+            const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+            const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+            const uint32_t n0 = hi1 ^ c1 ^ x0, n2 = hi0 ^ c3 ^ x1;
+            c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+            x0 += 0x9E3779B9u;
+            x1 += 0xBB67AE85u;
+        }
+        b0 = c0; b1 = c1; b2 = c2; b3 = c3;
+    }
+    __device__ __forceinline__ float uniform() {
+        const uint32_t w = draw & 3u;
+        if (w == 0u) block();
+        const uint32_t x = w == 0u ? b0 : (w == 1u ? b1 : (w == 2u ? b2 : b3));
+        draw++;
+        return (float)x * 0x1p-32f + 0x1p-33f;
+    }
 };
 
 // ------------------------------------------------------------------------ traversal
@@ -259,7 +288,8 @@ __device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, flo
 
 // ------------------------------------------------------------------------ BSDFs
 // utility.h:51-62 / 73-82; vec3(...) arguments drawn x, y, z in order.
-__device__ __forceinline__ float3 onUnitSphere(Xorwow& g) {
+template <class G>
+__device__ __forceinline__ float3 onUnitSphere(G& g) {
     float3 res;
     float norm;
     do {
@@ -271,7 +301,8 @@ __device__ __forceinline__ float3 onUnitSphere(Xorwow& g) {
     } while (norm >= 1.0f);
     return divs(res, sqrtf(norm));
 }
-__device__ __forceinline__ float3 inUnitSphere(Xorwow& g) {
+template <class G>
+__device__ __forceinline__ float3 inUnitSphere(G& g) {
     float3 res;
     do {
         float a = g.uniform() - 0.5f;
@@ -284,7 +315,8 @@ __device__ __forceinline__ float3 inUnitSphere(Xorwow& g) {
 __device__ __forceinline__ float3 reflect3(float3 v, float3 n) { return sub(v, scale(2.0f * dot3(v, n), n)); }
 
 // Material::scatter (material.h:28-61); returns false when the path is absorbed.
-__device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, float3& d, float3& atten, Xorwow& g) {
+template <class G>
+__device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, float3& d, float3& atten, G& g) {
     const float4 m0 = S.mats[2 * h.mat], m1 = S.mats[2 * h.mat + 1];
     const int type = (int)__float_as_uint(m1.y);
     if (type == PT_LAMBERTIAN) {
@@ -356,6 +388,11 @@ struct RenderParams {
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
     int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
+    // sample mode (RNG_SAMPLE): work unit = (tile, chunk of `chunk` samples); partial sums per
+    // chunk land in `partial` ([chunk][pixel] x 3 floats) and are reduced in chunk order.
+    int nchunks, chunk;
+    float* partial;
+    uint32_t seed0, seed1;
 };
 
 __device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
@@ -477,11 +514,17 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 // so primitive tests run with many lanes active instead of one or two.
 constexpr int kLeafQ = 4;
 
-template <int STACK>
+template <int STACK, bool SAMPLE>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
-    const int tile = tileOf(P, blockIdx.x);
+    // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
+    // sample mode: one wave = (tile, chunk): samples [chunk*C, chunk*C + C) of the tile's pixels.
+    const int unit = blockIdx.x;
+    const int tile = SAMPLE ? tileOf(P, unit / P.nchunks) : tileOf(P, unit);
+    const int chunkIdx = SAMPLE ? unit % P.nchunks : 0;
+    const int s0 = SAMPLE ? chunkIdx * P.chunk : 0;
+    const int nSamples = SAMPLE ? min(P.chunk, P.spp - s0) : P.spp;
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int col = tx * 8 + (lane & 7);
     const int lrow = ty * 8 + (lane >> 3);
@@ -497,8 +540,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
 
-    Xorwow g{0, 0, 0, 0, 0, 0};
-    if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+    using Gen = typename std::conditional<SAMPLE, Philox, Xorwow>::type;
+    Gen g{};
+    if constexpr (SAMPLE) {
+        g.k0 = P.seed0;
+        g.k1 = P.seed1;
+        g.pixel = (uint32_t)(valid ? globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0) * (uint32_t)P.width + (uint32_t)col;
+    } else {
+        if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+    }
     float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
@@ -530,6 +580,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
+        if constexpr (SAMPLE) { g.sample = (uint32_t)(s0 + sample); g.draw = 0u; }                \
         const float u_ = (fcol + g.uniform()) * P.invW;                                           \
         const float v_ = (frow + g.uniform()) * P.invH;                                           \
         o = P.cam.pos;                                                                            \
@@ -541,8 +592,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     bool started = false;
     if (valid) {
         if (P.max_depth <= 0) {
-            for (; sample < P.spp; sample++) { PT_NEW_PATH(); sum = add(sum, sky(d, att)); }
-        } else if (P.spp > 0) {
+            for (; sample < nSamples; sample++) { PT_NEW_PATH(); sum = add(sum, sky(d, att)); }
+        } else if (nSamples > 0) {
             PT_NEW_PATH();
             PT_BEGIN_RAY();
             active = true;
@@ -550,7 +601,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }
     }
     sRays += (uint32_t)__popcll(__ballot(started));
-    sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)P.spp : 0u);
+    sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
 
     for (;;) {
         const bool wantNode = node >= 0 && qn <= kLeafQ - 2;
@@ -640,7 +691,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
                 }
                 if (done) {
                     sum = add(sum, contrib);
-                    if (++sample == P.spp) {
+                    if (++sample == nSamples) {
                         active = false;
                     } else {
                         PT_NEW_PATH();
@@ -657,14 +708,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }
     }
     if (valid) {
-        float* outp = P.out + 3 * idx;   // main.cu:290-293
-        outp[0] = sqrtf(sum.x * P.invSpp);
-        outp[1] = sqrtf(sum.y * P.invSpp);
-        outp[2] = sqrtf(sum.z * P.invSpp);
-        P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+        if constexpr (SAMPLE) {
+            float* pp = P.partial + 3 * ((size_t)chunkIdx * (size_t)P.width * (size_t)P.nrows + idx);
+            pp[0] = sum.x; pp[1] = sum.y; pp[2] = sum.z;
+        } else {
+            float* outp = P.out + 3 * idx;   // main.cu:290-293
+            outp[0] = sqrtf(sum.x * P.invSpp);
+            outp[1] = sqrtf(sum.y * P.invSpp);
+            outp[2] = sqrtf(sum.z * P.invSpp);
+            P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+        }
     }
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
+    if (lane == 0) {
+        const unsigned dt = (unsigned)min(tEnd - tStart, 0xffffffffull);
+        if constexpr (SAMPLE) atomicAdd(P.tileCost + tile, dt);
+        else P.tileCost[tile] = dt;
+    }
     if (P.waveTimes && lane == 0) {
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -682,6 +742,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
 }
 #undef PT_BEGIN_RAY
 #undef PT_NEW_PATH
+
+// Sample mode epilogue: out = sqrt(sum over chunks (in order) of the chunk sums / spp).
+__global__ __launch_bounds__(256) void reduceChunksKernel(const float* __restrict__ partial, float* out, int64_t npix,
+                                                          int nchunks, float invSpp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    float x = 0.0f, y = 0.0f, z = 0.0f;
+    for (int c = 0; c < nchunks; c++) {
+        const float* q = partial + 3 * ((size_t)c * (size_t)npix + (size_t)i);
+        x = x + q[0];
+        y = y + q[1];
+        z = z + q[2];
+    }
+    out[3 * i + 0] = sqrtf(x * invSpp);
+    out[3 * i + 1] = sqrtf(y * invSpp);
+    out[3 * i + 2] = sqrtf(z * invSpp);
+}
 
 // 4-wide variant of renderKernelWF.  Wide node (128 B = 8 x float4): SoA child boxes
 // {minx[4]}{miny[4]}{minz[4]}{maxx[4]}{maxy[4]}{maxz[4]}, {ref[4]}, pad.  A wide node is a
@@ -1199,6 +1276,8 @@ struct pt_film {
     DevBuf jumps;   // XORWOW jump matrices (for pt_film_reset)
     DevBuf tileCost, tileOrder;   // measured per-tile cost of the last launch; LPT launch order
     bool haveOrder = false;
+    DevBuf partial;               // sample mode: per-chunk partial sums
+    size_t partialBytes = 0;
 };
 
 namespace {
@@ -1302,7 +1381,9 @@ int setDevice(int dev) {
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
     if (P.kernel == PT_KERNEL_WIDE) renderKernelW4<S><<<P.ntiles, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S><<<P.ntiles, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT && P.nchunks > 0)
+        renderKernelWF<S, true><<<P.ntiles * P.nchunks, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
 }
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
@@ -1740,7 +1821,19 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
         return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
     if (kernel == PT_KERNEL_WIDE && s->nobj > 1 && !s->wide.p) return fail(PT_ERR_STATE, "wide BVH missing");
+    const int rng = opts ? opts->rng : PT_RNG_COMPAT;
+    if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
+    if (rng == PT_RNG_SAMPLE && kernel != PT_KERNEL_WAVEFRONT) {
+        if (opts && opts->kernel != PT_KERNEL_DEFAULT)
+            return fail(PT_ERR_INVALID, "pt_render_ex: sample mode runs on the wavefront kernel");
+        kernel = PT_KERNEL_WAVEFRONT;
+    }
     P.kernel = kernel;
+    P.nchunks = 0;
+    P.chunk = 0;
+    P.partial = nullptr;
+    P.seed0 = (uint32_t)f->seed;
+    P.seed1 = (uint32_t)(f->seed >> 32);
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64) : envInt("PT_LEAF_BATCH", 8);
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64) : envInt("PT_SHADE_BATCH", 16);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
@@ -1750,10 +1843,22 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4))) return rc;
         f->haveOrder = false;
     }
-    const bool lpt = !(opts && opts->reserved == 1);   // reserved == 1: identity order (A/B)
+    const bool lpt = !(opts && (opts->flags & PT_RENDER_IDENTITY_ORDER));
+    if (rng == PT_RNG_SAMPLE && np > 0) {
+        P.chunk = (opts && opts->chunk > 0) ? opts->chunk : 64;
+        P.nchunks = (spp + P.chunk - 1) / P.chunk;
+        const size_t need = (size_t)P.nchunks * (size_t)np * 12;
+        if (f->partialBytes < need) {
+            if ((rc = devAlloc(f->partial, need))) return rc;
+            f->partialBytes = need;
+        }
+        P.partial = f->partial.as<float>();
+        if ((int64_t)f->height * f->width >= (1ll << 32)) return fail(PT_ERR_INVALID, "frame too large for sample mode");
+    }
     P.tileCost = f->tileCost.as<unsigned>();
     P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
     P.prioTiles = P.tileOrder ? envInt("PT_PRIO_TILES", 1024) : 0;
+    if (P.nchunks > 0) HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // accumulated per chunk
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
@@ -1769,6 +1874,10 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (P.ntiles > 0 && (rc = dispatchRender(stack, P, st))) {
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
         return rc;
+    }
+    if (P.nchunks > 0) {
+        reduceChunksKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(P.partial, dst, np, P.nchunks, P.invSpp);
+        HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));

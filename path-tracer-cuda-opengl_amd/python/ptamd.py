@@ -51,7 +51,12 @@ class Stats(C.Structure):
 
 
 class RenderOpts(C.Structure):
-    _fields_ = [("kernel", C.c_int32), ("leaf_batch", C.c_int32), ("shade_batch", C.c_int32), ("reserved", C.c_int32)]
+    _fields_ = [("kernel", C.c_int32), ("leaf_batch", C.c_int32), ("shade_batch", C.c_int32), ("flags", C.c_int32),
+                ("rng", C.c_int32), ("chunk", C.c_int32), ("reserved0", C.c_int32), ("reserved1", C.c_int32)]
+
+
+RNG_COMPAT, RNG_SAMPLE = 0, 1
+IDENTITY_ORDER = 1
 
 
 KERNEL_DEFAULT, KERNEL_SIMPLE, KERNEL_WAVEFRONT, KERNEL_WIDE = 0, 1, 2, 3
@@ -295,12 +300,13 @@ class Film:
 
 
 def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, out=None, stream=None,
-           kernel: int = KERNEL_DEFAULT, leaf_batch: int = 0, shade_batch: int = 0):
+           kernel: int = KERNEL_DEFAULT, leaf_batch: int = 0, shade_batch: int = 0, rng: int = RNG_COMPAT,
+           chunk: int = 0, flags: int = 0):
     """Render spp samples per pixel of the film's rows.  `out` may be a numpy array (host) or
     an integer device pointer (then `stream` is a hipStream_t handle or None).  Returns
     (rgb or None, Stats)."""
     st = Stats()
-    opts = RenderOpts(kernel, leaf_batch, shade_batch, 0)
+    opts = RenderOpts(kernel, leaf_batch, shade_batch, flags, rng, chunk, 0, 0)
     if out is None or isinstance(out, np.ndarray):
         rgb = out if out is not None else np.zeros((film.n_pixels, 3), np.float32)
         _check(lib.pt_render_ex(scene.h, film.h, C.byref(camera), spp, max_depth, _ptr(rgb), 0, None, C.byref(opts),

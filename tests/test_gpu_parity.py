@@ -315,3 +315,96 @@ def test_lpt_tile_order_is_result_neutral(pt, gpu):
         frames.append(rgb.copy())
     for fr in frames[1:]:
         np.testing.assert_array_equal(bits(fr), bits(frames[0]))
+
+
+# ---------------------------------------------------------------------------------------------
+# Sample mode (PT_RNG_SAMPLE): Philox per pixel-sample, (tile, chunk) work units.
+# ---------------------------------------------------------------------------------------------
+
+def render_sample_both(pt, orc, gpu, p, w, h, spp, depth, seed, chunk, **kw):
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, seed, device=gpu, **kw)
+    rgb, st = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    ref, rst = orc.render_sample(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, f.rows, spp,
+                                 depth, seed, chunk or 64, nthreads=8)
+    return rgb, st, ref, rst, s, f
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth,chunk", [
+    ("rtiow", 64, 36, 5, 50, 2),             # ragged last chunk
+    ("triangle_world", 80, 45, 4, 50, 0),    # default chunk (64) > spp: one chunk
+    ("cornell", 64, 64, 9, 8, 4),
+    ("bunny_cornell", 96, 54, 6, 50, 1),     # one sample per work unit
+    ("bunny_cornell", 37, 19, 3, 50, 3),     # ragged tiles
+])
+def test_sample_mode_bit_exact(pt, orc, gpu, name, w, h, spp, depth, chunk, monkeypatch):
+    for leaf, shade in (("8", "16"), ("1", "1")):
+        monkeypatch.setenv("PT_LEAF_BATCH", leaf)
+        monkeypatch.setenv("PT_SHADE_BATCH", shade)
+        p = pt.Preset(name, w, h)
+        rgb, st, ref, rst, _, f = render_sample_both(pt, orc, gpu, p, w, h, spp, depth, 11, chunk)
+        np.testing.assert_array_equal(bits(rgb), bits(ref))
+        assert st.rays == rst.rays and st.paths == rst.paths == w * h * spp
+        assert st.tri_tests == rst.tri_tests and st.sphere_tests == rst.sphere_tests
+
+
+def test_sample_mode_stateless_and_stripes(pt, orc, gpu):
+    """Sample mode is a pure function of (seed, pixel, sample): repeated calls agree, the film's
+    XORWOW streams are untouched, and stripe partitions reassemble the full frame."""
+    w, h, spp = 50, 30, 4
+    p = pt.Preset("bunny_cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, 3, device=gpu)
+    init = f.get_rng()
+    a, _ = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=2)
+    b, _ = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=2)
+    np.testing.assert_array_equal(bits(a), bits(b))
+    np.testing.assert_array_equal(f.get_rng(), init)
+    full = a.reshape(h, w, 3)
+    for parts, stripe in ((2, 8), (3, 3)):
+        img = np.zeros_like(full)
+        for part in range(parts):
+            fp = pt.Film(w, h, 3, device=gpu, stripe_height=stripe, n_parts=parts, part=part)
+            rgb, _ = pt.render(s, fp, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=2)
+            img[fp.rows] = rgb.reshape(fp.n_rows, w, 3)
+        np.testing.assert_array_equal(bits(img), bits(full))
+    # compat mode after sample mode still starts from the untouched streams
+    c, _ = pt.render(s, f, p.camera, 1, 50)
+    f.reset()
+    d, _ = pt.render(s, f, p.camera, 1, 50)
+    np.testing.assert_array_equal(bits(c), bits(d))
+
+
+def test_sample_mode_options(pt, gpu):
+    p = pt.Preset("cornell", 16, 16)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(16, 16, 1, device=gpu)
+    with pytest.raises(pt.PtError):
+        pt.render(s, f, p.camera, 1, 5, rng=5)
+    with pytest.raises(pt.PtError):   # sample mode runs on the wavefront kernel only
+        pt.render(s, f, p.camera, 1, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_SIMPLE)
+    a, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WAVEFRONT)
+    b, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE)
+    np.testing.assert_array_equal(bits(a), bits(b))
+    z, st = pt.render(s, f, p.camera, 2, 0, rng=pt.RNG_SAMPLE)   # depth 0: black, no rays
+    assert st.rays == 0 and not z.any()
+
+
+def test_sample_mode_full_size_c3_statistics(pt, orc, gpu):
+    """C3 at full size: sample mode and compat mode are two estimates of the same image."""
+    p = pt.Preset("bunny_cornell")
+    w, h = p.width, p.height
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    a, sa = pt.render(s, pt.Film(w, h, 1, device=gpu), p.camera, 16, p.max_depth)
+    b, sb = pt.render(s, pt.Film(w, h, 2, device=gpu), p.camera, 16, p.max_depth, rng=pt.RNG_SAMPLE, chunk=4)
+    la = (a.astype(np.float64) ** 2).reshape(h // 40, 40, w // 40, 40, 3).mean(axis=(1, 3))
+    lb = (b.astype(np.float64) ** 2).reshape(h // 40, 40, w // 40, 40, 3).mean(axis=(1, 3))
+    assert np.abs(la - lb).mean() < 0.01 * max(la.mean(), 1e-3) + 0.002
+    assert abs(sa.rays / sa.paths - sb.rays / sb.paths) < 0.02 * (sa.rays / sa.paths)
+    # rows through the oracle
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    rows = np.array([3, 700], np.int32)
+    ref, _ = orc.render_sample(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, rows, 16,
+                               p.max_depth, 2, 4, 8)
+    np.testing.assert_array_equal(bits(b.reshape(h, w, 3)[rows].reshape(-1, 3)), bits(ref))

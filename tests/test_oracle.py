@@ -182,3 +182,37 @@ def test_render_threads_deterministic(pt, orc):
     a, _ = orc.render(p.objects, p.materials, nodes, cam, 40, 24, rows, 3, 50, orc.film_states(3, 40, rows), 1)
     b, _ = orc.render(p.objects, p.materials, nodes, cam, 40, 24, rows, 3, 50, orc.film_states(3, 40, rows), 8)
     np.testing.assert_array_equal(a, b)
+
+
+def test_philox_known_answers(orc):
+    """Philox4x32-10 known-answer vectors (Salmon et al., Random123 kat_vectors): the sample-mode
+    generator maps counter = {draw/4, sample, pixel_lo, pixel_hi}, key = {seed_lo, seed_hi}."""
+    assert [orc.philox_word(0, 0, 0, d) for d in range(4)] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    seed = (0x299f31d0 << 32) | 0xa4093822
+    pixel = (0x03707344 << 32) | 0x13198a2e
+    got = [orc.philox_word(seed, 0x85a308d3, pixel, 4 * 0x243f6a88 + d) for d in range(4)]
+    assert got == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_sample_mode_statistical_parity(pt, orc):
+    """Sample mode (Philox per pixel-sample) renders the same image as the reference's
+    integrator: against exp2.png with the compat-mode bound, and chunking is sum-order only."""
+    p = pt.Preset("triangle_world", 1200, 675)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects))
+    rows = np.arange(675)
+    cam = pt.camera_to_array(p.camera)
+    nt = os.cpu_count() or 4
+    rgb, st = orc.render_sample(p.objects, p.materials, nodes, cam, 1200, 675, rows, 4, 50, seed=7, chunk=2,
+                                nthreads=nt)
+    lin = (rgb.astype(np.float64) ** 2).reshape(27, 25, 48, 25, 3).mean(axis=(1, 3))
+    diff = np.abs(lin - np.load(os.path.join(GOLDEN, "exp2_blocks.npy")))
+    assert diff.mean() < 0.006, diff.mean()
+    assert diff.max() < 0.05, diff.max()
+    assert abs(st.rays / st.paths - 2.908) < 0.03
+    # chunk size changes only the summation grouping: identical ray counts, near-identical pixels
+    small = np.arange(0, 675, 45)
+    a, sa = orc.render_sample(p.objects, p.materials, nodes, cam, 1200, 675, small, 4, 50, 7, 2, nt)
+    b, sb = orc.render_sample(p.objects, p.materials, nodes, cam, 1200, 675, small, 4, 50, 7, 64, nt)
+    assert sa.rays == sb.rays and sa.tri_tests == sb.tri_tests
+    np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
+    np.testing.assert_array_equal(a, rgb.reshape(675, 1200, 3)[small].reshape(-1, 3))
