@@ -152,9 +152,12 @@ int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int
  *   pixel, curand_init(seed, pixel, 0), samples consumed in order and kept across calls like
  *   the reference's devStates; a pixel's samples are inherently sequential.
  *   PT_RNG_SAMPLE: one counter-based Philox4x32-10 stream per pixel-sample (key = film seed,
- *   counter = {draw/4, sample, pixel}); work units are (8x8 tile, chunk of `chunk` samples)
- *   (0 = 64), chunk sums are added in chunk order.  Deterministic, statistically identical to
- *   the reference, not its random numbers; does not advance the film's XORWOW streams.
+ *   counter = {draw/4, sample, pixel}); samples are summed in blocks of `chunk` samples
+ *   (0 = max(16, ceil(spp/64))) and the block sums are added in order.  Blocks are grouped
+ *   into work units (waves) from the previous launch's per-tile costs; the grouping never
+ *   changes the image.  Deterministic, statistically identical to the reference, not its
+ *   random numbers; does not advance the film's XORWOW streams.  Needs chunk-count x pixels
+ *   x 12 bytes of device memory for the block sums.
  * leaf_batch / shade_batch: wavefront thresholds in lanes (0 = default).
  * flags: PT_RENDER_IDENTITY_ORDER disables the longest-tile-first launch order. */
 enum { PT_KERNEL_DEFAULT = 0, PT_KERNEL_SIMPLE = 1, PT_KERNEL_WAVEFRONT = 2, PT_KERNEL_WIDE = 3 };

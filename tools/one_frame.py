@@ -1,0 +1,21 @@
+"""Render one frame (profiling target).  usage: python tools/one_frame.py [c2|c3|c5] [spp] [compat|sample] [chunk]"""
+import json
+import os
+import sys
+
+import torch  # noqa: F401
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"))
+import ptamd  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+spp = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+rng = ptamd.RNG_SAMPLE if len(sys.argv) > 3 and sys.argv[3] == "sample" else ptamd.RNG_COMPAT
+chunk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg])
+scene = ptamd.Scene(p.objects, p.materials)
+film = ptamd.Film(p.width, p.height, 1)
+_, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=chunk)
+print(json.dumps({"cfg": cfg, "spp": spp, "kernel_ms": st.kernel_ms, "rays": st.rays, "node_visits": st.node_visits,
+                  "tri_tests": st.tri_tests}))

@@ -39,7 +39,8 @@ def main():
     scene = ptamd.Scene(p.objects, p.materials)
     film = ptamd.Film(p.width, p.height, 1)
     os.environ["PT_WAVE_TIMES"] = out
-    rgb, st = ptamd.render(scene, film, p.camera, spp, p.max_depth)
+    rng = ptamd.RNG_SAMPLE if os.environ.get("RNG") == "sample" else ptamd.RNG_COMPAT
+    rgb, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=int(os.environ.get("CHUNK", "0")))
     t = np.fromfile(out, dtype=np.uint64).reshape(-1, 3)
     print(json.dumps({"config": cfg, "spp": spp, "kernel_ms": st.kernel_ms, **analyse(t, 5 * 1024)}))
 
