@@ -57,7 +57,8 @@ for name, res, args in [
                               C.c_int, _P, _P, C.POINTER(Stats), C.c_int, _P]),
     ("orc_render_sample", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
                                     C.c_int, C.c_uint64, C.c_int, _P, C.POINTER(Stats), C.c_int]),
-    ("orc_philox_word", C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]),
+    ("orc_philox_word", C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int]),
+    ("orc_sample_stream", None, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_void_p]),
     ("orc_render", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
                              C.c_int, _P, _P, C.POINTER(Stats), C.c_int]),
 ]:
@@ -209,6 +210,13 @@ def film_states(seed: int, width: int, rows) -> np.ndarray:
     return out
 
 
-def philox_word(seed: int, sample: int, pixel: int, draw: int) -> int:
-    """Sample-mode generator: uniform draw `draw` of pixel-sample (pixel, sample)."""
-    return int(lib.orc_philox_word(seed, sample, pixel, draw))
+def philox_word(key: int, counter, word: int) -> int:
+    """Philox4x32-10 output word `word` of block (counter[0..3], key)."""
+    return int(lib.orc_philox_word(key, *[int(c) for c in counter], word))
+
+
+def sample_stream(seed: int, sample: int, pixel: int) -> np.ndarray:
+    """Sample-mode XORWOW state {d, v0..v4} of pixel-sample (pixel, sample)."""
+    st = np.zeros(6, np.uint32)
+    lib.orc_sample_stream(seed, sample, pixel, _ptr(st))
+    return st

@@ -275,8 +275,6 @@ struct XorwowRng {
 };
 
 // Philox4x32-10 (Salmon et al. 2011; the generator cuRAND offers as curandStatePhilox4_32_10).
-// Sample mode stream of pixel p, sample s: key = seed, counter = {block, s, p_lo, p_hi}; draw i
-// is word (i % 4) of block (i / 4).  Uniform mapping as curand_uniform: u * 2^-32 + 2^-33.
 inline void philoxBlock(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t out[4]) {
     for (int r = 0; r < 10; r++) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
@@ -289,17 +287,16 @@ inline void philoxBlock(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-struct PhiloxRng {
-    uint32_t k0, k1, sample, p0, p1, draw = 0;
-    uint32_t buf[4] = {0, 0, 0, 0};
-    float operator()() {
-        if ((draw & 3u) == 0) philoxBlock(draw >> 2, sample, p0, p1, k0, k1, buf);
-        const uint32_t x = buf[draw & 3u];
-        draw++;
-        const float k = 2.3283064e-10f;
-        return (float)x * k + (k / 2.0f);
-    }
-};
+// Sample mode stream of (pixel p, sample s): one Philox block, key = seed, counter =
+// {s, p_lo, p_hi, "SAMP"}, seeds a XORWOW state {d, v0..v4} whose draws follow (curand_uniform).
+inline void sampleStream(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t st[6]) {
+    uint32_t w[4];
+    philoxBlock(sample, (uint32_t)pixel, (uint32_t)(pixel >> 32), 0x53414D50u, (uint32_t)seed, (uint32_t)(seed >> 32), w);
+    st[0] = w[3];
+    st[1] = w[0]; st[2] = w[1]; st[3] = w[2];
+    st[4] = w[3] ^ 0x6C078965u;
+    st[5] = w[0] ^ w[1] ^ 0x2545F491u;
+}
 struct TapeRng {
     const float* tape; int len; int pos;
     float operator()() { return pos < len ? tape[pos++] : (pos++, 0.5f); }
@@ -765,8 +762,9 @@ int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* 
                 for (int c0 = 0; c0 < spp; c0 += chunk) {   // chunks summed in order
                     V3 part{0, 0, 0};
                     for (int s = c0; s < std::min(spp, c0 + chunk); s++) {
-                        PhiloxRng rng{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)s, (uint32_t)pixel,
-                                      (uint32_t)(pixel >> 32)};
+                        uint32_t st[6];
+                        sampleStream(seed, (uint32_t)s, pixel, st);
+                        XorwowRng rng{st};
                         part = part + tracePath(objs, nobj, mats, nodes, cam, col, row, invW, invH, max_depth, rng, local);
                     }
                     total = total + part;
@@ -794,11 +792,14 @@ int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* 
     return 0;
 }
 
-uint32_t orc_philox_word(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t draw) {
-    PhiloxRng rng{(uint32_t)seed, (uint32_t)(seed >> 32), sample, (uint32_t)pixel, (uint32_t)(pixel >> 32)};
+uint32_t orc_philox_word(uint64_t key, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, int word) {
     uint32_t out[4];
-    philoxBlock(draw >> 2, sample, (uint32_t)pixel, (uint32_t)(pixel >> 32), rng.k0, rng.k1, out);
-    return out[draw & 3u];
+    philoxBlock(c0, c1, c2, c3, (uint32_t)key, (uint32_t)(key >> 32), out);
+    return out[word & 3];
+}
+
+void orc_sample_stream(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t state[6]) {
+    sampleStream(seed, sample, pixel, state);
 }
 
 }  // extern "C"

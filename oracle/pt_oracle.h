@@ -77,14 +77,15 @@ int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, 
                 const int32_t* rows, int nrows, int spp, int max_depth,
                 uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays);
 
-/* Sample mode: one Philox4x32-10 stream per pixel-sample (key = seed, counter = {draw/4,
- * sample, pixel_lo, pixel_hi}); samples summed per chunk of `chunk` samples, chunk sums
- * summed in order, sqrt(total / spp).  Same rows/out layout as orc_render. */
+/* Sample mode: pixel-sample (p, s) draws from a XORWOW state seeded by one Philox4x32-10
+ * block (key = seed, counter = {s, p_lo, p_hi, "SAMP"}); samples summed per chunk of `chunk`
+ * samples, chunk sums summed in order, sqrt(total / spp).  Same rows/out layout as orc_render. */
 int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
                       const orc_node* nodes, const orc_camera* cam, int width, int height,
                       const int32_t* rows, int nrows, int spp, int max_depth, uint64_t seed, int chunk,
                       float* out_rgb, orc_stats* stats, int nthreads);
-uint32_t orc_philox_word(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t draw);
+uint32_t orc_philox_word(uint64_t key, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, int word);
+void orc_sample_stream(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t state[6]);  /* {d, v0..v4} */
 
 #ifdef __cplusplus
 }

@@ -100,33 +100,23 @@ struct Xorwow {
     __device__ __forceinline__ float uniform() { return (float)next() * 0x1p-32f + 0x1p-33f; }
 };
 
-// Philox4x32-10 (Salmon et al. 2011), the counter-based generator of sample mode: the stream
-// of (pixel p, sample s) is key = seed, counter = {draw / 4, s, p_lo, p_hi}; draw i is word
-// i % 4 of block i / 4; uniform mapping as curand_uniform.  Any sample can start anywhere.
-struct Philox {
-    uint32_t k0, k1, sample, pixel, draw;
-    uint32_t b0, b1, b2, b3;
-    __device__ __forceinline__ void block() {
-        uint32_t c0 = draw >> 2, c1 = sample, c2 = pixel, c3 = 0u, x0 = k0, x1 = k1;
-#pragma unroll
-        for (int r = 0; r < 10; r++) {
-            const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-            const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-            const uint32_t n0 = hi1 ^ c1 ^ x0, n2 = hi0 ^ c3 ^ x1;
-            c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-            x0 += 0x9E3779B9u;
-            x1 += 0xBB67AE85u;
-        }
-        b0 = c0; b1 = c1; b2 = c2; b3 = c3;
+// Sample mode stream of (pixel p, sample s): one Philox4x32-10 block (Salmon et al. 2011)
+// with key = seed and counter = {s, p_lo, p_hi, "SAMP"} seeds a XORWOW state, whose draws
+// then cost a few shifts each (the reference's generator family, curand_uniform mapping).
+// Any sample of any pixel starts anywhere, in one block of work.
+__device__ __forceinline__ Xorwow sampleStream(uint32_t k0, uint32_t k1, uint32_t sample, uint32_t pixel) {
+    uint32_t c0 = sample, c1 = pixel, c2 = 0u, c3 = 0x53414D50u;
+#pragma unroll 1   // (a rolled loop keeps register pressure at the camera-ray site low)
+    for (int r = 0; r < 10; r++) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
     }
-    __device__ __forceinline__ float uniform() {
-        const uint32_t w = draw & 3u;
-        if (w == 0u) block();
-        const uint32_t x = w == 0u ? b0 : (w == 1u ? b1 : (w == 2u ? b2 : b3));
-        draw++;
-        return (float)x * 0x1p-32f + 0x1p-33f;
-    }
-};
+    return Xorwow{c3, c0, c1, c2, c3 ^ 0x6C078965u, c0 ^ c1 ^ 0x2545F491u};
+}
 
 // ------------------------------------------------------------------------ traversal
 // aabb::hit (aabb.h:21-34): per axis t0=(min-o)*inv, t1=(max-o)*inv, swap if inv<0,
@@ -143,6 +133,24 @@ __device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx,
     float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
     float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
     return !(hi < lo);
+}
+
+// slab() that also returns the entry distance lo = max(tmin, near planes).  For a box that
+// passed with tmax = T, the same test with any tmax' <= T fails iff tmax' < lo: hi(T') =
+// fminf(T', far planes) and fminf ignores NaN, so hi(T') < lo <=> T' < lo or far < lo, and
+// the latter is false because the box passed.  (lo is never NaN: fmaxf(tmin, NaN) = tmin.)
+struct SlabHit { bool hit; float lo; };
+__device__ __forceinline__ SlabHit slabLo(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                                          float3 o, float3 inv, float tmin, float tmax) {
+    float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
+    float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
+    float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
+    float nx = inv.x < 0.0f ? t1x : t0x, fx = inv.x < 0.0f ? t0x : t1x;
+    float ny = inv.y < 0.0f ? t1y : t0y, fy = inv.y < 0.0f ? t0y : t1y;
+    float nz = inv.z < 0.0f ? t1z : t0z, fz = inv.z < 0.0f ? t0z : t1z;
+    float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
+    float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
+    return SlabHit{!(hi < lo), lo};
 }
 
 // Primitive record (leaf order), 3 x float4:
@@ -389,13 +397,14 @@ struct RenderParams {
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
     int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
     // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples; the sum
-    // of block b lands in partial[b][pixel] (3 floats) and blocks are reduced in order, so the
-    // image does not depend on how blocks are grouped into work units.  Work unit i (one wave)
-    // = units[i] = {tile, first sample (a multiple of block), sample count, -}.
+    // of block b lands in partial[b][pixel] (3 floats) and blocks are reduced in order.  Each
+    // (pixel, block) is one task, summed in sample order by whichever lane takes it, so the
+    // image does not depend on scheduling.
     int nblocks, block;
     float* partial;
-    const int4* units;
-    int nunits;
+    unsigned* taskCounter;                    // next task (zeroed before the launch)
+    uint32_t ntasks;                          // tile slots x nblocks x 64
+    int nwaves;                               // persistent waves launched
     uint32_t seed0, seed1;
 };
 
@@ -517,42 +526,46 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 // reference order; node visit counts may be higher.  Lanes keep traversing while leaves wait,
 // so primitive tests run with many lanes active instead of one or two.
 constexpr int kLeafQ = 4;
+#ifndef PT_WAVES_PER_EU
+#define PT_WAVES_PER_EU 4
+#endif
 
 template <int STACK, bool SAMPLE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void renderKernelWF(RenderParams P) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
-    // sample mode: one wave = one work unit: samples [s0, s0 + n) of one tile's pixels.
-    int tile, s0 = 0, nSamples = P.spp;
-    if constexpr (SAMPLE) {
-        const int4 u = P.units[blockIdx.x];
-        tile = u.x; s0 = u.y; nSamples = u.z;
-    } else {
-        tile = tileOf(P, blockIdx.x);
+    // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
+    // block) from a global counter and sums that block's samples in order (see PT_TAKE_TASKS).
+    // `sample` runs to nSamples (compat: spp; sample mode: the end of the task's block, and
+    // `sample` is the absolute sample index)
+    int tile = SAMPLE ? -1 : tileOf(P, blockIdx.x), nSamples = SAMPLE ? 0 : P.spp;
+    int col = 0, lrow = 0;
+    if constexpr (!SAMPLE) {
+        col = (tile % P.tiles_x) * 8 + (lane & 7);
+        lrow = (tile / P.tiles_x) * 8 + (lane >> 3);
     }
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    const int col = tx * 8 + (lane & 7);
-    const int lrow = ty * 8 + (lane >> 3);
-    const bool valid = col < P.width && lrow < P.nrows;
-    const size_t idx = valid ? (size_t)lrow * P.width + col : 0;
+    bool valid = !SAMPLE && col < P.width && lrow < P.nrows;
+    uint32_t idx = valid ? (uint32_t)lrow * (uint32_t)P.width + (uint32_t)col : 0u;   // npix < 2^32
     const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
-    if ((int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
-    const float fcol = (float)col;
-    const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
+    if (!SAMPLE && (int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
+    float fcol = (float)col;
+    float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
     uint32_t* my = stk + lane;
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
+#ifdef PT_DIAG
+    uint32_t itN = 0, itL = 0, itS = 0, sPops = 0;   // scheduler diagnostics (iterations per kind)
+#define PT_DIAG_ADD(v, x) (v) += (x)
+#else
+#define PT_DIAG_ADD(v, x) ((void)0)
+#endif
 
-    using Gen = typename std::conditional<SAMPLE, Philox, Xorwow>::type;
-    Gen g{};
-    if constexpr (SAMPLE) {
-        g.k0 = P.seed0;
-        g.k1 = P.seed1;
-        g.pixel = (uint32_t)(valid ? globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0) * (uint32_t)P.width + (uint32_t)col;
-    } else {
+    Xorwow g{};
+    uint32_t cr = 0;     // sample mode: the task's pixel, col | local row << 16
+    if constexpr (!SAMPLE) {
         if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
     }
     float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
@@ -560,13 +573,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     float closest = 0.0f;
     int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
     uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: leaf refs in DFS order
+    float l0 = 0.0f, l1 = 0.0f, l2 = 0.0f, l3 = 0.0f;   // their slab entry distances
     bool active = false;
+    // sample mode task state: summation block, its tile (cost accounting), rays traced for it
+    uint32_t taskRays = 0, depthPaths = 0;
+    bool needTask = SAMPLE;
 
     // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
     // captured variables address-taken and they end up in scratch memory.)
 #define PT_BEGIN_RAY()                                                                              \
     do {                                                                                          \
         depthLeft--;                                                                              \
+        if constexpr (SAMPLE) taskRays++;                                                         \
         closest = __builtin_inff();                                                               \
         best = -1;                                                                                \
         sp = 0;                                                                                   \
@@ -584,21 +602,70 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }                                                                                         \
     } while (0)
     // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
-    // Sample mode: close the summation block when sample s0+sample-1 was its last.
-#define PT_FLUSH_BLOCK()                                                                            \
+    // Sample mode: lanes with needTask take the next tasks of the global counter (one atomic
+    // per wave).  Task t = (tile slot t / 64 / nblocks in launch order, block (t / 64) % nblocks,
+    // pixel t % 64 of the 8x8 tile); tasks off the frame edge are skipped.  Sets `got` for lanes
+    // that received a task; lanes that find the counter exhausted stop asking.
+#define PT_TAKE_TASKS(got)                                                                          \
     do {                                                                                          \
-        if constexpr (SAMPLE) {                                                                   \
-            if ((s0 + sample) % P.block == 0 || sample == nSamples) {                             \
-                float* pp_ = P.partial + 3 * ((size_t)((s0 + sample - 1) / P.block) *             \
-                                              ((size_t)P.width * (size_t)P.nrows) + idx);         \
-                pp_[0] = sum.x; pp_[1] = sum.y; pp_[2] = sum.z;                                   \
-                sum = f3(0.0f, 0.0f, 0.0f);                                                       \
+        for (;;) {                                                                                \
+            const uint64_t m_ = __ballot(needTask);                                               \
+            if (m_ == 0) break;                                                                   \
+            const int leader_ = __ffsll((unsigned long long)m_) - 1;                              \
+            uint32_t b_ = 0;                                                                      \
+            if (lane == leader_) b_ = atomicAdd(P.taskCounter, (uint32_t)__popcll(m_));           \
+            /* wave-uniform: the taken tasks span task groups (tile slot, block) g0 and g0 + 1 */ \
+            const uint32_t base_ = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_)); \
+            const uint32_t g0_ = base_ >> 6, off_ = base_ & 63u;                                  \
+            const uint32_t slotA_ = g0_ / (uint32_t)P.nblocks, blkA_ = g0_ - slotA_ * (uint32_t)P.nblocks; \
+            const bool wrap_ = blkA_ + 1u == (uint32_t)P.nblocks;                                  \
+            const uint32_t slotB_ = wrap_ ? slotA_ + 1u : slotA_, blkB_ = wrap_ ? 0u : blkA_ + 1u; \
+            const uint32_t nslots_ = (uint32_t)P.ntiles;                                          \
+            const uint32_t tA_ = slotA_ < nslots_ ? (P.tileOrder ? (uint32_t)P.tileOrder[slotA_] : slotA_) : 0u; \
+            const uint32_t tB_ = slotB_ < nslots_ ? (P.tileOrder ? (uint32_t)P.tileOrder[slotB_] : slotB_) : 0u; \
+            const uint32_t tyA_ = tA_ / (uint32_t)P.tiles_x, txA_ = tA_ - tyA_ * (uint32_t)P.tiles_x; \
+            const uint32_t tyB_ = tB_ / (uint32_t)P.tiles_x, txB_ = tB_ - tyB_ * (uint32_t)P.tiles_x; \
+            if (needTask) {                                                                       \
+                const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));             \
+                if (base_ + k_ >= P.ntasks) {                                                     \
+                    needTask = false;                                                             \
+                } else {                                                                          \
+                    const uint32_t o_ = off_ + k_, px_ = o_ & 63u;                                \
+                    const bool hi_ = o_ >= 64u;                                                   \
+                    const int c_ = (int)((hi_ ? txB_ : txA_) * 8u + (px_ & 7u));                  \
+                    const int r_ = (int)((hi_ ? tyB_ : tyA_) * 8u + (px_ >> 3));                  \
+                    if (c_ < P.width && r_ < P.nrows) {                                           \
+                        needTask = false;                                                         \
+                        got = true;                                                               \
+                        taskRays = 0;                                                             \
+                        cr = (uint32_t)c_ | ((uint32_t)r_ << 16);                                 \
+                        frow = (float)globalRow(r_, P.stripe_h, P.nparts, P.part);                \
+                        sample = (int)(hi_ ? blkB_ : blkA_) * P.block;                            \
+                        nSamples = min(sample + P.block, P.spp);                                  \
+                        sum = f3(0.0f, 0.0f, 0.0f);                                               \
+                    }                                                                             \
+                }                                                                                 \
             }                                                                                     \
         }                                                                                         \
     } while (0)
+    // Sample mode: the lane's block is complete -> its sum, cost; ask for the next task.
+#define PT_FINISH_TASK()                                                                            \
+    do {                                                                                          \
+        const uint32_t blk_ = (uint32_t)(nSamples - 1) / (uint32_t)P.block;                        \
+        const uint32_t c_ = cr & 0xffffu, r_ = cr >> 16;                                          \
+        float* pp_ = P.partial + 3 * ((size_t)blk_ * ((size_t)P.width * (size_t)P.nrows) +        \
+                                      (size_t)(r_ * (uint32_t)P.width + c_));                     \
+        pp_[0] = sum.x; pp_[1] = sum.y; pp_[2] = sum.z;                                           \
+        atomicAdd(P.tileCost + (r_ >> 3) * (uint32_t)P.tiles_x + (c_ >> 3), taskRays + 1u);       \
+        needTask = true;                                                                          \
+    } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
-        if constexpr (SAMPLE) { g.sample = (uint32_t)(s0 + sample); g.draw = 0u; }                \
+        if constexpr (SAMPLE) {                                                                   \
+            fcol = (float)(cr & 0xffffu);                                                         \
+            g = sampleStream(P.seed0, P.seed1, (uint32_t)sample,                                  \
+                             (uint32_t)frow * (uint32_t)P.width + (cr & 0xffffu));                \
+        }                                                                                         \
         const float u_ = (fcol + g.uniform()) * P.invW;                                           \
         const float v_ = (frow + g.uniform()) * P.invH;                                           \
         o = P.cam.pos;                                                                            \
@@ -608,13 +675,31 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
     } while (0)
 
     bool started = false;
-    if (valid) {
+    if constexpr (SAMPLE) {
+        // Every lane starts with needTask: the first loop iteration is a SHADE step that hands
+        // out tasks.  max_depth <= 0 (no bounce: each sample is the sky colour of its camera
+        // ray) is handled here, without the loop.
         if (P.max_depth <= 0) {
-            while (sample < nSamples) {
+            for (;;) {
+                bool got = false;
+                PT_TAKE_TASKS(got);
+                if (__ballot(got) == 0) break;
+                if (got) {
+                    depthPaths += (uint32_t)(nSamples - sample);
+                    for (; sample < nSamples; sample++) {
+                        PT_NEW_PATH();
+                        sum = add(sum, sky(d, att));
+                    }
+                    PT_FINISH_TASK();
+                }
+            }
+            needTask = false;
+        }
+    } else if (valid) {
+        if (P.max_depth <= 0) {
+            for (; sample < nSamples; sample++) {
                 PT_NEW_PATH();
                 sum = add(sum, sky(d, att));
-                sample++;
-                PT_FLUSH_BLOCK();
             }
         } else if (nSamples > 0) {
             PT_NEW_PATH();
@@ -624,12 +709,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }
     }
     sRays += (uint32_t)__popcll(__ballot(started));
-    sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
+    sPaths += (uint32_t)__popcll(__ballot(started)) +
+              (!SAMPLE && P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
 
     for (;;) {
         const bool wantNode = node >= 0 && qn <= kLeafQ - 2;
         const bool wantLeaf = qn > 0;
-        const bool wantShade = active && node < 0 && qn == 0;
+        const bool wantShade = (active && node < 0 && qn == 0) || needTask;
         const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
@@ -642,22 +728,33 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         if (kind == 0) {
             // ------------------------------------------------------------------ NODE
             sVisits += (uint32_t)nN;
+            PT_DIAG_ADD(itN, 1u);
+#ifdef PT_PAD_NODE   // experiment: extra dependent VALU work per NODE iteration
+            if (wantNode) {
+                float x_ = inv.x;
+#pragma unroll
+                for (int i_ = 0; i_ < PT_PAD_NODE; i_++) x_ = x_ * 1.0000001f + 1e-30f;
+                if (x_ == 12345.678f) atomicOr(S.err, 4u);
+            }
+#endif
             if (wantNode) {
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
                 const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
-                const bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest);
-                const bool hr = slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest);
-                // append hit leaves in order (left, then right)
-                if (hl && (lref & kLeafBit)) {
+                const SlabHit hl = slabLo(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest);
+                const SlabHit hr = slabLo(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest);
+                // append hit leaves in order (left, then right) with their slab entry distances
+                if (hl.hit && (lref & kLeafBit)) {
                     q0 = qn == 0 ? lref : q0; q1 = qn == 1 ? lref : q1; q2 = qn == 2 ? lref : q2; q3 = qn == 3 ? lref : q3;
+                    l0 = qn == 0 ? hl.lo : l0; l1 = qn == 1 ? hl.lo : l1; l2 = qn == 2 ? hl.lo : l2; l3 = qn == 3 ? hl.lo : l3;
                     qn++;
                 }
-                if (hr && (rref & kLeafBit)) {
+                if (hr.hit && (rref & kLeafBit)) {
                     q0 = qn == 0 ? rref : q0; q1 = qn == 1 ? rref : q1; q2 = qn == 2 ? rref : q2; q3 = qn == 3 ? rref : q3;
+                    l0 = qn == 0 ? hr.lo : l0; l1 = qn == 1 ? hr.lo : l1; l2 = qn == 2 ? hr.lo : l2; l3 = qn == 3 ? hr.lo : l3;
                     qn++;
                 }
-                const bool il = hl && !(lref & kLeafBit), ir = hr && !(rref & kLeafBit);
+                const bool il = hl.hit && !(lref & kLeafBit), ir = hr.hit && !(rref & kLeafBit);
                 // push left then right, pop: descend straight into the child that would be popped
                 if (ir) {
                     if (il) {
@@ -677,16 +774,29 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         } else if (kind == 1) {
             // ------------------------------------------------------------------ LEAF
             bool tested = false, sph = false;
+            PT_DIAG_ADD(itL, 1u);
+            PT_DIAG_ADD(sPops, (uint32_t)nL);
+#ifdef PT_PAD_LEAF   // experiment: extra dependent VALU work per LEAF iteration
+            if (wantLeaf) {
+                float x_ = inv.x;
+#pragma unroll
+                for (int i_ = 0; i_ < PT_PAD_LEAF; i_++) x_ = x_ * 1.0000001f + 1e-30f;
+                if (x_ == 12345.678f) atomicOr(S.err, 4u);
+            }
+#endif
             if (wantLeaf) {
                 const uint32_t ref = q0;
+                const float lo = l0;
                 q0 = q1; q1 = q2; q2 = q3;
+                l0 = l1; l1 = l2; l2 = l3;
                 qn--;
                 const uint32_t k = ref & kPrimMask;
                 sph = (ref & kSphereBit) != 0;
-                const Prim pr = loadPrim(S, k);
-                if (primBoxHit(pr, sph, o, inv, 0.001f, closest)) {
+                // Exact re-test of the leaf box with the current closest: the box passed when it
+                // was queued, with a tmax >= closest, so now it fails iff closest < lo (slabLo).
+                if (!(closest < lo)) {
                     tested = true;
-                    const float t = primHitT(pr, sph, o, d, 0.001f, closest);
+                    const float t = primHitT(loadPrim(S, k), sph, o, d, 0.001f, closest);
                     if (t >= 0.0f) { closest = t; best = (int)k; }
                 }
             }
@@ -695,7 +805,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         } else {
             // ------------------------------------------------------------------ SHADE
             bool newRay = false, newSample = false;
-            if (wantShade) {
+            PT_DIAG_ADD(itS, 1u);
+            if (wantShade && !needTask) {
                 bool done = false;
                 float3 contrib = f3(0.0f, 0.0f, 0.0f);
                 if (best < 0) {
@@ -715,24 +826,32 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
                 if (done) {
                     sum = add(sum, contrib);
                     ++sample;
-                    PT_FLUSH_BLOCK();
                     if (sample == nSamples) {
                         active = false;
+                        if constexpr (SAMPLE) PT_FINISH_TASK();
                     } else {
-                        PT_NEW_PATH();
-                        PT_BEGIN_RAY();
-                        newRay = newSample = true;
+                        newSample = true;
                     }
-                } else {
-                    PT_BEGIN_RAY();
-                    newRay = true;
+                }
+                newRay = true;   // bounce, next sample (newSample) or finished (reset below)
+                if (!active) newRay = false;
+            }
+            if constexpr (SAMPLE) {   // idle lanes take new tasks and start their first path
+                bool got = false;
+                PT_TAKE_TASKS(got);
+                if (got) {
+                    active = true;
+                    newRay = newSample = true;
                 }
             }
+            // one camera-ray and one ray-start site for every lane that needs them
+            if (newSample) PT_NEW_PATH();
+            if (newRay) PT_BEGIN_RAY();
             sRays += (uint32_t)__popcll(__ballot(newRay));
             sPaths += (uint32_t)__popcll(__ballot(newSample));
         }
     }
-    if constexpr (!SAMPLE) {   // (sample mode: every block was flushed when it closed)
+    if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
         if (valid) {
             float* outp = P.out + 3 * idx;   // main.cu:290-293
             outp[0] = sqrtf(sum.x * P.invSpp);
@@ -742,10 +861,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }
     }
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) {
-        const unsigned dt = (unsigned)min(tEnd - tStart, 0xffffffffull);
-        if constexpr (SAMPLE) atomicAdd(P.tileCost + tile, dt);
-        else P.tileCost[tile] = dt;
+    if (!SAMPLE && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
+    if constexpr (SAMPLE) {   // max_depth <= 0: paths counted per lane
+        if (P.max_depth <= 0) waveReduceAdd(P.counters + 4, depthPaths);
     }
     if (P.waveTimes && lane == 0) {
         unsigned xcc;
@@ -760,11 +878,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         atomicAdd(P.counters + 2, (unsigned long long)sTris);
         atomicAdd(P.counters + 3, (unsigned long long)sSph);
         atomicAdd(P.counters + 4, (unsigned long long)sPaths);
+#ifdef PT_DIAG
+        atomicAdd(P.counters + 8, (unsigned long long)itN);
+        atomicAdd(P.counters + 9, (unsigned long long)itL);
+        atomicAdd(P.counters + 10, (unsigned long long)itS);
+        atomicAdd(P.counters + 11, (unsigned long long)sPops);
+#endif
     }
 }
 #undef PT_BEGIN_RAY
 #undef PT_NEW_PATH
-#undef PT_FLUSH_BLOCK
+#undef PT_TAKE_TASKS
+#undef PT_FINISH_TASK
+#undef PT_DIAG_ADD
 
 // Sample mode epilogue: out = sqrt(sum over blocks (in order) of the block sums / spp).
 __global__ __launch_bounds__(256) void reduceChunksKernel(const float* __restrict__ partial, float* out, int64_t npix,
@@ -1265,7 +1391,11 @@ int envInt(const char* name, int dflt) {
 
 int stackFor(int depth) {
     const int need = depth + 1;
+#ifdef PT_STACK24
+    for (int s : {16, 24, 32, 48, 64, 80})
+#else
     for (int s : {16, 32, 48, 64, 80})
+#endif
         if (need <= s) return s;
     return -1;
 }
@@ -1301,10 +1431,9 @@ struct pt_film {
     bool haveOrder = false;
     std::vector<unsigned> cost;   // host copy of tileCost and the spp it was measured at
     int costSpp = 0;
-    DevBuf partial, units;        // sample mode: per-block partial sums; work-unit list
-    size_t partialBytes = 0, unitBytes = 0;
-    std::vector<int4> hostUnits;
-    int cus = 0;                  // compute units of the device (work-unit sizing)
+    DevBuf partial, taskCounter;  // sample mode: per-block partial sums; task counter
+    size_t partialBytes = 0;
+    int cus = 0;                  // compute units of the device (persistent grid size)
 };
 
 namespace {
@@ -1408,14 +1537,17 @@ int setDevice(int dev) {
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
     if (P.kernel == PT_KERNEL_WIDE) renderKernelW4<S><<<P.ntiles, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WAVEFRONT && P.units)
-        renderKernelWF<S, true><<<P.nunits, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
+        renderKernelWF<S, true><<<P.nwaves, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
 }
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
     switch (stack) {
         case 16: launchRender<16>(P, st); break;
+#ifdef PT_STACK24
+        case 24: launchRender<24>(P, st); break;
+#endif
         case 32: launchRender<32>(P, st); break;
         case 48: launchRender<48>(P, st); break;
         case 64: launchRender<64>(P, st); break;
@@ -1430,6 +1562,9 @@ int dispatchTrace(int stack, const DevScene& S, const pt_ray* r, int64_t n, floa
     const unsigned blocks = (unsigned)((n + kWave - 1) / kWave);
     switch (stack) {
         case 16: traceKernel<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+#ifdef PT_STACK24
+        case 24: traceKernel<24><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+#endif
         case 32: traceKernel<32><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
         case 48: traceKernel<48><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
         case 64: traceKernel<64><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
@@ -1517,7 +1652,7 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
     }
     if ((rc = devAlloc(s->mats, m.size() * sizeof(float4)))) return rc;
     HIP_TRY(hipMemcpy(s->mats.p, m.data(), m.size() * sizeof(float4), hipMemcpyHostToDevice));
-    if ((rc = devAlloc(s->counters, 8 * sizeof(unsigned long long)))) return rc;
+    if ((rc = devAlloc(s->counters, 16 * sizeof(unsigned long long)))) return rc;
     *out = s.release();
     return PT_OK;
 }
@@ -1691,7 +1826,7 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     DevBuf dr, dh;
     if ((rc = devAlloc(dr, n * sizeof(pt_ray))) || (rc = devAlloc(dh, n * sizeof(pt_hit)))) return rc;
     if (n > 0) HIP_TRY(hipMemcpy(dr.p, rays, n * sizeof(pt_ray), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(s->counters.p, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->counters.p, 0, 16 * sizeof(unsigned long long)));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -1708,7 +1843,7 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (n > 0) HIP_TRY(hipMemcpy(hits, dh.p, n * sizeof(pt_hit), hipMemcpyDeviceToHost));
-    unsigned long long c[8] = {0};
+    unsigned long long c[16] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     c[4] = 0;
     fillStats(stats, c, ms);
@@ -1791,56 +1926,6 @@ int pt_film_set_rng(pt_film* f, const uint32_t* states) {
     return PT_OK;
 }
 
-namespace {
-// Sample-mode work units.  A unit is one wave: a tile and a run of whole summation blocks.
-// Without measured costs every tile is cut into runs of ~256 samples.  With the costs of the
-// previous launch (per tile, scaled to this spp), a tile is cut into k = ceil(cost / U) runs,
-// U = total cost / (wave slots x PT_UNIT_SPLIT), and units are launched longest first: cheap
-// tiles stay one wave (no per-wave overhead), the few expensive tiles (paths trapped under
-// the bunny, ~40 rays per path) spread over many waves and start first.  Results never depend
-// on the cut (blocks are summed in order by reduceChunksKernel).
-void buildUnits(pt_film* f, const RenderParams& P, int spp, bool useCosts) {
-    std::vector<int4>& u = f->hostUnits;
-    u.clear();
-    const int B = P.block, nb = P.nblocks, nt = P.ntiles;
-    auto cut = [&](int t, int k) {   // tile t into k runs of whole blocks
-        for (int g = 0; g < k; g++) {
-            const int b0 = (int)((int64_t)g * nb / k), b1 = (int)((int64_t)(g + 1) * nb / k);
-            if (b1 > b0) u.push_back(make_int4(t, b0 * B, std::min(spp, b1 * B) - b0 * B, 0));
-        }
-    };
-    const bool haveCosts = useCosts && f->costSpp > 0 && (int)f->cost.size() == nt;
-    if (!haveCosts) {
-        const int per = std::max(1, std::min(nb, 256 / B));
-        for (int t = 0; t < nt; t++) cut(t, (nb + per - 1) / per);
-        return;
-    }
-    if (!f->cus) {
-        if (hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device) != hipSuccess) f->cus = 256;
-        f->cus = std::max(f->cus, 1);
-    }
-    const double scale = (double)spp / (double)f->costSpp;
-    double total = 0;
-    for (int t = 0; t < nt; t++) total += (double)f->cost[t] * scale + 1.0;
-    const double slots = (double)f->cus * 4 * 5;   // 4 SIMDs x 5 waves (96 VGPRs)
-    const double U = std::max(1.0, total / (slots * std::max(1, envInt("PT_UNIT_SPLIT", 4))));
-    std::vector<double> est;
-    for (int t = 0; t < nt; t++) {
-        const double c = (double)f->cost[t] * scale + 1.0;
-        const int k = (int)std::min<double>(nb, std::max(1.0, std::ceil(c / U)));
-        const size_t first = u.size();
-        cut(t, k);
-        for (size_t i = first; i < u.size(); i++) est.push_back(c * u[i].z / spp);
-    }
-    std::vector<int> order(u.size());
-    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return est[a] > est[b]; });
-    std::vector<int4> sorted(u.size());
-    for (size_t i = 0; i < order.size(); i++) sorted[i] = u[order[i]];
-    u.swap(sorted);
-}
-}  // namespace
-
 int pt_render(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max_depth, float* out, int on_dev,
               void* stream, pt_stats* stats) {
     return pt_render_ex(s, f, cam, spp, max_depth, out, on_dev, stream, nullptr, stats);
@@ -1864,7 +1949,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = devAlloc(dout, (size_t)std::max<int64_t>(1, np) * 12))) return rc;
         dst = dout.as<float>();
     }
-    HIP_TRY(hipMemsetAsync(s->counters.p, 0, 8 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16 * sizeof(unsigned long long), st));
     RenderParams P;
     P.S = devScene(s);
     P.cam.pos = make_float3(cam->origin[0], cam->origin[1], cam->origin[2]);
@@ -1909,8 +1994,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.nblocks = 0;
     P.block = 0;
     P.partial = nullptr;
-    P.units = nullptr;
-    P.nunits = 0;
+    P.taskCounter = nullptr;
+    P.ntasks = 0;
+    P.nwaves = 0;
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64) : envInt("PT_LEAF_BATCH", 8);
@@ -1925,7 +2011,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     const bool lpt = !(opts && (opts->flags & PT_RENDER_IDENTITY_ORDER));
     const bool sample = rng == PT_RNG_SAMPLE && np > 0 && P.ntiles > 0;
     if (sample) {
-        if ((int64_t)f->height * f->width >= (1ll << 32)) return fail(PT_ERR_INVALID, "frame too large for sample mode");
+        if (f->width >= 65536 || f->nrows >= 65536)
+            return fail(PT_ERR_INVALID, "sample mode: frame width and rows must be < 65536");
         P.block = (opts && opts->chunk > 0) ? opts->chunk : std::max(16, (spp + 63) / 64);
         P.nblocks = (spp + P.block - 1) / P.block;
         const size_t need = (size_t)P.nblocks * (size_t)np * 12;
@@ -1934,25 +2021,30 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
             f->partialBytes = need;
         }
         P.partial = f->partial.as<float>();
-        buildUnits(f, P, spp, lpt);
-        P.nunits = (int)f->hostUnits.size();
-        const size_t ub = f->hostUnits.size() * sizeof(int4);
-        if (f->unitBytes < ub) {
-            if ((rc = devAlloc(f->units, ub))) return rc;
-            f->unitBytes = ub;
+        const uint64_t ntasks = (uint64_t)P.ntiles * (uint64_t)P.nblocks * 64u;
+        if (ntasks >= (1ull << 32) - 4096)
+            return fail(PT_ERR_INVALID, "sample mode: too many (pixel, block) tasks; raise the block size (chunk)");
+        P.ntasks = (uint32_t)ntasks;
+        if (!f->taskCounter.p && (rc = devAlloc(f->taskCounter, 64))) return rc;
+        HIP_TRY(hipMemsetAsync(f->taskCounter.p, 0, 4, st));
+        P.taskCounter = f->taskCounter.as<unsigned>();
+        if (!f->cus) {
+            if (hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device) != hipSuccess)
+                f->cus = 256;
+            f->cus = std::max(f->cus, 1);
         }
-        // hostUnits stays untouched until the next call, which starts after this one synchronised
-        HIP_TRY(hipMemcpyAsync(f->units.p, f->hostUnits.data(), ub, hipMemcpyHostToDevice, st));
-        P.units = f->units.as<int4>();
-        HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // accumulated over a tile's units
+        // persistent: enough waves to fill every SIMD (4 per CU, PT_WAVES_PER_EU each)
+        const uint64_t full = (uint64_t)f->cus * 4 * PT_WAVES_PER_EU;
+        P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
+        HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
     }
     P.tileCost = f->tileCost.as<unsigned>();
-    P.tileOrder = (!sample && lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
-    P.prioTiles = (P.tileOrder || (sample && f->costSpp > 0 && lpt)) ? envInt("PT_PRIO_TILES", 1024) : 0;
+    P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
+    P.prioTiles = (P.tileOrder && !sample) ? envInt("PT_PRIO_TILES", 1024) : 0;
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
-    const size_t nwaves = sample ? (size_t)P.nunits : ntl;   // = grid size
+    const size_t nwaves = sample ? (size_t)P.nwaves : ntl;   // = grid size
     if (timesPath && *timesPath && kernel != PT_KERNEL_SIMPLE) {
         if ((rc = devAlloc(dtimes, nwaves * 24))) return rc;
         HIP_TRY(hipMemsetAsync(dtimes.p, 0, nwaves * 24, st));
@@ -1996,9 +2088,13 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         }
     }
     if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * 12, hipMemcpyDeviceToHost));
-    unsigned long long c[8] = {0};
+    unsigned long long c[16] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     fillStats(stats, c, ms);
+    if (std::getenv("PT_ITER_STATS") && c[8] + c[9] + c[10] > 0)   // diagnostic: wavefront scheduler
+        std::fprintf(stderr, "[pt] iterations node %llu leaf %llu shade %llu | lanes/iter node %.1f leaf %.1f "
+                     "shade %.1f\n", c[8], c[9], c[10], (double)c[1] / std::max(1ull, c[8]),
+                     (double)c[11] / std::max(1ull, c[9]), (double)c[0] / std::max(1ull, c[10]));
     if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
     return PT_OK;
 }

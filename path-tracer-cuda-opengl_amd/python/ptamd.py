@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libpt.so")
+LIB_PATH = os.environ.get("PT_LIB") or os.path.join(PKG, "libpt.so")   # PT_LIB: A/B builds
 MODELS_DIR = os.path.join(REPO, "models")
 
 PT_OK = 0

@@ -410,20 +410,18 @@ def test_sample_mode_full_size_c3_statistics(pt, orc, gpu):
     np.testing.assert_array_equal(bits(b.reshape(h, w, 3)[rows].reshape(-1, 3)), bits(ref))
 
 
-def test_sample_mode_unit_split_is_result_neutral(pt, gpu, monkeypatch):
-    """Work units (how a tile's summation blocks are grouped into waves) come from the previous
-    launch's tile costs; any grouping gives the identical frame."""
+def test_sample_mode_scheduling_is_result_neutral(pt, gpu):
+    """Lanes take (pixel, block) tasks dynamically, in a tile order taken from the previous
+    launch's costs; any schedule gives the identical frame."""
     w, h, spp = 96, 54, 40
     p = pt.Preset("bunny_cornell", w, h)
     s = pt.Scene(p.objects, p.materials, device=gpu)
     f = pt.Film(w, h, 8, device=gpu)
     ref, _ = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=4, flags=pt.IDENTITY_ORDER)
-    for split in ("1", "4", "100000"):   # 100000: every block its own wave
-        monkeypatch.setenv("PT_UNIT_SPLIT", split)
-        for _ in range(2):   # first launch after a mode/spp change may use uniform units
-            rgb, st = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=4)
-            np.testing.assert_array_equal(bits(rgb), bits(ref))
-    # a different spp reuses the costs scaled; still identical to a fresh film
+    for _ in range(3):   # 2nd and 3rd launch: longest tiles first
+        rgb, st = pt.render(s, f, p.camera, spp, 50, rng=pt.RNG_SAMPLE, chunk=4)
+        np.testing.assert_array_equal(bits(rgb), bits(ref))
+    # a different spp after costs were measured: identical to a fresh film
     a, _ = pt.render(s, f, p.camera, 7, 50, rng=pt.RNG_SAMPLE, chunk=2)
     b, _ = pt.render(s, pt.Film(w, h, 8, device=gpu), p.camera, 7, 50, rng=pt.RNG_SAMPLE, chunk=2)
     np.testing.assert_array_equal(bits(a), bits(b))

@@ -185,13 +185,25 @@ def test_render_threads_deterministic(pt, orc):
 
 
 def test_philox_known_answers(orc):
-    """Philox4x32-10 known-answer vectors (Salmon et al., Random123 kat_vectors): the sample-mode
-    generator maps counter = {draw/4, sample, pixel_lo, pixel_hi}, key = {seed_lo, seed_hi}."""
-    assert [orc.philox_word(0, 0, 0, d) for d in range(4)] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
-    seed = (0x299f31d0 << 32) | 0xa4093822
-    pixel = (0x03707344 << 32) | 0x13198a2e
-    got = [orc.philox_word(seed, 0x85a308d3, pixel, 4 * 0x243f6a88 + d) for d in range(4)]
-    assert got == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+    """Philox4x32-10 known-answer vectors (Salmon et al., Random123 kat_vectors)."""
+    assert [orc.philox_word(0, (0, 0, 0, 0), w) for w in range(4)] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    ff = 0xffffffff
+    assert [orc.philox_word((ff << 32) | ff, (ff, ff, ff, ff), w) for w in range(4)] == \
+        [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    key = (0x299f31d0 << 32) | 0xa4093822
+    assert [orc.philox_word(key, (0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), w) for w in range(4)] == \
+        [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+def test_sample_stream_seeding(orc):
+    """Sample-mode stream of (pixel, sample) = XORWOW seeded from one Philox block with counter
+    {sample, pixel_lo, pixel_hi, 'SAMP'}; distinct pixel-samples get distinct states."""
+    seed, sample, pixel = 0x1234_5678_9abc_def0, 7, 123456
+    w = [orc.philox_word(seed, (sample, pixel, 0, 0x53414D50), k) for k in range(4)]
+    st = orc.sample_stream(seed, sample, pixel)
+    assert list(st) == [w[3], w[0], w[1], w[2], w[3] ^ 0x6C078965, w[0] ^ w[1] ^ 0x2545F491]
+    states = {tuple(orc.sample_stream(seed, s, p)) for s in range(8) for p in range(64)}
+    assert len(states) == 8 * 64
 
 
 def test_sample_mode_statistical_parity(pt, orc):

@@ -16,6 +16,8 @@ chunk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg])
 scene = ptamd.Scene(p.objects, p.materials)
 film = ptamd.Film(p.width, p.height, 1)
-_, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=chunk)
+for _ in range(int(os.environ.get("REPEAT", "1"))):   # later launches use measured tile costs
+    film.reset()
+    _, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=chunk)
 print(json.dumps({"cfg": cfg, "spp": spp, "kernel_ms": st.kernel_ms, "rays": st.rays, "node_visits": st.node_visits,
                   "tri_tests": st.tri_tests}))

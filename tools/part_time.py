@@ -1,0 +1,32 @@
+"""Frame time of one rank's share (part p of n stripes) on one GPU: predicts the multi-GPU frame
+time without a multi-GPU box.  usage: python tools/part_time.py [n_parts] [compat|sample] [spp]"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"))
+import ptamd  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+mode = sys.argv[2] if len(sys.argv) > 2 else "sample"
+spp = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
+rng = ptamd.RNG_SAMPLE if mode == "sample" else ptamd.RNG_COMPAT
+p = ptamd.Preset("bunny_cornell")
+scene = ptamd.Scene(p.objects, p.materials)
+for part in sorted({0, n // 2, n - 1}):
+    f = ptamd.Film(p.width, p.height, 1, stripe_height=8, n_parts=n, part=part)
+    out = torch.empty((f.n_pixels * 3,), dtype=torch.float32, device="cuda")
+    times = []
+    for it in range(3):
+        f.reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, st = ptamd.render(scene, f, p.camera, spp, p.max_depth, out=out.data_ptr(), rng=rng)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    print(json.dumps({"n_parts": n, "part": part, "mode": mode, "ms": [round(t * 1e3, 1) for t in times],
+                      "rays": st.rays}), flush=True)
