@@ -8,6 +8,14 @@ the N ranks (stripe s -> rank s % N), so the total work is fixed as N grows ("st
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5] [--spp S]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+RNG mode (--rng): `sample` (default) draws each pixel-sample from its own XORWOW stream seeded
+by Philox, so a frame is a set of independent (pixel, 16-sample block) tasks that persistent
+waves take from a counter: every GPU gets an equal share.  `compat` reproduces the reference's
+per-pixel curand_init(seed, pixel, 0) streams bit for bit; a pixel's 1024 samples are then one
+sequential chain, and the slowest pixels (paths trapped under the bunny, ~40 rays each) bound
+the frame at ~1.8 s however many GPUs share it.  At N = 1 the line also carries one compat frame
+(`compat_mode`).  Both modes render the same image in distribution (tests/test_oracle.py).
+
 Rank 0 prints one JSON line.  `value` = total closest-hit queries (counted in-kernel, all
 ranks) / max-over-ranks wall time of the K timed frames.  `roofline.achieved` = algorithmic
 bytes (56 B per internal-node visit + 40 B per triangle test + 20 B per sphere
@@ -76,10 +84,12 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--leaf-batch", type=int, default=0, help="wavefront LEAF threshold (0 = library default)")
     ap.add_argument("--shade-batch", type=int, default=0, help="wavefront SHADE threshold (0 = library default)")
-    ap.add_argument("--rng", default="compat", choices=["compat", "sample"],
-                    help="compat: the reference's per-pixel cuRAND-XORWOW streams (bit-exact parity mode); "
-                         "sample: Philox per pixel-sample, (tile, sample-chunk) work units")
-    ap.add_argument("--chunk", type=int, default=0, help="sample mode: samples per work unit (0 = library default)")
+    ap.add_argument("--rng", default="sample", choices=["compat", "sample"],
+                    help="sample (default): a XORWOW stream per pixel-sample seeded by Philox, (pixel, block) "
+                         "tasks on persistent waves -- the frame splits over any number of GPUs; compat: the "
+                         "reference's per-pixel cuRAND-XORWOW streams (a pixel's 1024 samples are sequential)")
+    ap.add_argument("--chunk", type=int, default=0, help="sample mode: summation block (0 = library default)")
+    ap.add_argument("--no-compat", action="store_true", help="skip the compat-mode reference frame (N = 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,7 +133,7 @@ def main() -> None:
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
     # Sample mode runs on the wavefront kernel only: its own counters are used (they include the
-    # speculative node visits, +0.27% on C3 in compat mode, so `achieved` is overstated by that).
+    # speculative node visits, +0.3% on C3 in compat mode, so `achieved` is overstated by that).
     ref_st = frame() if sample else frame(ptamd.KERNEL_SIMPLE)
     for _ in range(max(0, args.warmup - 1)):
         frame()
@@ -157,6 +167,23 @@ def main() -> None:
     else:
         total_rays = float(rays)
 
+    compat = None
+    if sample and world == 1 and not args.no_compat:
+        # the reference's RNG semantics on the same frame, for comparison (2 frames: the first
+        # measures tile costs for the longest-first launch order, the second is timed)
+        for it in range(2):
+            film.reset(stream.cuda_stream)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            _, cst = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
+                                  stream=stream.cuda_stream, rng=ptamd.RNG_COMPAT)
+            torch.cuda.synchronize(dev)
+            el1 = time.perf_counter() - t1
+        compat = {"value": cst.rays / el1 / 1e6, "unit": "Mray/s", "ms_per_step": el1 * 1e3,
+                  "kernel_ms": cst.kernel_ms, "rays_per_frame": cst.rays,
+                  "note": "compat RNG mode (per-pixel curand_init(seed, pixel, 0) streams, bit-exact with "
+                          "oracle/), one frame after one warmup"}
+
     if rank == 0:
         if world > 1:   # un-permute the stripes of the last frame (rank 0 holds the full image)
             ptdist.assemble(gathered, h, w, STRIPE, world)
@@ -178,8 +205,8 @@ def main() -> None:
             "config": {"workload": workload, "width": w, "height": h, "spp": spp, "max_depth": depth,
                        "stripe_rows": STRIPE, "parallelism": f"rows{world}",
                        "rays_per_frame": total_rays / args.steps,
-                       "rng": ("Philox4x32-10 per pixel-sample (sample mode), chunk "
-                               f"{args.chunk or 64}") if sample else
+                       "rng": ("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
+                               f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
                               "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -189,9 +216,11 @@ def main() -> None:
                                                "node visits)") if sample else
                                               ("reference-order traversal counts of the same frame "
                                                "(ray-synchronous kernel, warmup step 1)"),
-                         "node_visits_reference": ref_st.node_visits,
+                         "node_visits_reference": None if sample else ref_st.node_visits,
                          "node_visits_wavefront": spec_visits / args.steps},
         }
+        if compat:
+            out["compat_mode"] = compat
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(preset)
         print(json.dumps(out), flush=True)

@@ -10,7 +10,7 @@ TAG=${TAG:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 BENCH_ARGS=${BENCH_ARGS:-}
-PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline}
+PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-compat}
 step() {  # name, limit, command...
     local name=$1 lim=$2; shift 2
     timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1
