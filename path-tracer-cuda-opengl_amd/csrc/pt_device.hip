@@ -525,7 +525,10 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 // add visits.  So the sequence of primitive tests -- and every pixel -- is identical to the
 // reference order; node visit counts may be higher.  Lanes keep traversing while leaves wait,
 // so primitive tests run with many lanes active instead of one or two.
-constexpr int kLeafQ = 4;
+#ifndef PT_LEAF_QUEUE
+#define PT_LEAF_QUEUE 4
+#endif
+constexpr int kLeafQ = PT_LEAF_QUEUE;
 #ifndef PT_WAVES_PER_EU
 #define PT_WAVES_PER_EU 4
 #endif
@@ -572,8 +575,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
     int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
-    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: leaf refs in DFS order
-    float l0 = 0.0f, l1 = 0.0f, l2 = 0.0f, l3 = 0.0f;   // their slab entry distances
+    uint32_t qref[kLeafQ];   // leaf queue: leaf refs in DFS order (registers: constant indices only)
+    float lq[kLeafQ];     // their slab entry distances
+#pragma unroll
+    for (int i = 0; i < kLeafQ; i++) { qref[i] = 0u; lq[i] = 0.0f; }
     bool active = false;
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
     uint32_t taskRays = 0, depthPaths = 0;
@@ -745,13 +750,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 const SlabHit hr = slabLo(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest);
                 // append hit leaves in order (left, then right) with their slab entry distances
                 if (hl.hit && (lref & kLeafBit)) {
-                    q0 = qn == 0 ? lref : q0; q1 = qn == 1 ? lref : q1; q2 = qn == 2 ? lref : q2; q3 = qn == 3 ? lref : q3;
-                    l0 = qn == 0 ? hl.lo : l0; l1 = qn == 1 ? hl.lo : l1; l2 = qn == 2 ? hl.lo : l2; l3 = qn == 3 ? hl.lo : l3;
+#pragma unroll
+                    for (int i = 0; i < kLeafQ; i++) {
+                        qref[i] = qn == i ? lref : qref[i];
+                        lq[i] = qn == i ? hl.lo : lq[i];
+                    }
                     qn++;
                 }
                 if (hr.hit && (rref & kLeafBit)) {
-                    q0 = qn == 0 ? rref : q0; q1 = qn == 1 ? rref : q1; q2 = qn == 2 ? rref : q2; q3 = qn == 3 ? rref : q3;
-                    l0 = qn == 0 ? hr.lo : l0; l1 = qn == 1 ? hr.lo : l1; l2 = qn == 2 ? hr.lo : l2; l3 = qn == 3 ? hr.lo : l3;
+#pragma unroll
+                    for (int i = 0; i < kLeafQ; i++) {
+                        qref[i] = qn == i ? rref : qref[i];
+                        lq[i] = qn == i ? hr.lo : lq[i];
+                    }
                     qn++;
                 }
                 const bool il = hl.hit && !(lref & kLeafBit), ir = hr.hit && !(rref & kLeafBit);
@@ -785,10 +796,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             }
 #endif
             if (wantLeaf) {
-                const uint32_t ref = q0;
-                const float lo = l0;
-                q0 = q1; q1 = q2; q2 = q3;
-                l0 = l1; l1 = l2; l2 = l3;
+                const uint32_t ref = qref[0];
+                const float lo = lq[0];
+#pragma unroll
+                for (int i = 0; i + 1 < kLeafQ; i++) { qref[i] = qref[i + 1]; lq[i] = lq[i + 1]; }
                 qn--;
                 const uint32_t k = ref & kPrimMask;
                 sph = (ref & kSphereBit) != 0;
@@ -1999,8 +2010,15 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.nwaves = 0;
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
-    P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64) : envInt("PT_LEAF_BATCH", 8);
-    P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64) : envInt("PT_SHADE_BATCH", 16);
+    // Defaults swept on C3 (tools/gpu_variants.sh): compat mode is bound by its slowest pixels'
+    // sequential chains, so lanes must not wait long (6 / 12: 1,716 ms vs 1,836 at 8 / 16);
+    // sample mode is throughput-bound and prefers fuller LEAF / SHADE steps (24 / 32: 1,741 ->
+    // 1,326..1,355 ms).
+    const bool sampleRng = rng == PT_RNG_SAMPLE;
+    P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
+                                                 : envInt("PT_LEAF_BATCH", sampleRng ? 24 : 6);
+    P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
+                                                   : envInt("PT_SHADE_BATCH", sampleRng ? 32 : 12);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
     const int stack = s->nobj > 1 ? stackFor(kernel == PT_KERNEL_WIDE ? s->wideDepth : s->depth) : 16;
     const size_t ntl = (size_t)std::max(1, P.ntiles);

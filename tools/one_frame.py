@@ -9,7 +9,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"))
 import ptamd  # noqa: E402
 
-cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+cfg = os.environ.get("CFG") or (sys.argv[1] if len(sys.argv) > 1 else "c3")
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 rng = ptamd.RNG_SAMPLE if len(sys.argv) > 3 and sys.argv[3] == "sample" else ptamd.RNG_COMPAT
 chunk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
