@@ -132,9 +132,7 @@ def main() -> None:
     # order exactly: its counters give the frame's ALGORITHMIC bytes (the wavefront kernel may
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
-    # Sample mode runs on the wavefront kernel only: its own counters are used (they include the
-    # speculative node visits, +0.3% on C3 in compat mode, so `achieved` is overstated by that).
-    ref_st = frame() if sample else frame(ptamd.KERNEL_SIMPLE)
+    ref_st = frame(ptamd.KERNEL_SIMPLE)
     for _ in range(max(0, args.warmup - 1)):
         frame()
     if world > 1:
@@ -212,11 +210,9 @@ def main() -> None:
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
                          "algo_bytes_per_launch": kbytes / args.steps,
-                         "algo_bytes_source": ("wavefront-kernel counters of the same frame (incl. speculative "
-                                               "node visits)") if sample else
-                                              ("reference-order traversal counts of the same frame "
-                                               "(ray-synchronous kernel, warmup step 1)"),
-                         "node_visits_reference": None if sample else ref_st.node_visits,
+                         "algo_bytes_source": "reference-order traversal counts of the same frame "
+                                              "(ray-synchronous kernel, warmup step 1)",
+                         "node_visits_reference": ref_st.node_visits,
                          "node_visits_wavefront": spec_visits / args.steps},
         }
         if compat:

@@ -428,7 +428,10 @@ __device__ __forceinline__ void waveReduceAdd(unsigned long long* dst, uint32_t 
     if ((threadIdx.x & (kWave - 1)) == 0 && x) atomicAdd(dst, x);
 }
 
-template <int STACK>
+// SAMPLE: the sample-mode streams and block sums, one wave per tile, samples in order -- the
+// same frame as renderKernelWF<STACK, true>, in the reference's traversal order (the bench
+// counts algorithmic bytes with it).
+template <int STACK, bool SAMPLE>
 __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
@@ -443,13 +446,16 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
     if (valid) {
         const size_t idx = (size_t)lrow * P.width + col;
         const int row = globalRow(lrow, P.stripe_h, P.nparts, P.part);
-        Xorwow g{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+        Xorwow g{};
+        if constexpr (!SAMPLE) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+        const uint32_t gpix = (uint32_t)row * (uint32_t)P.width + (uint32_t)col;
         const float fcol = (float)col, frow = (float)row;
         float3 sum = f3(0.0f, 0.0f, 0.0f);
         float3 o, d, att;
         int depthLeft = 0, sample = 0;
         // newPath: main.cu:284-286 + camera::get_ray (camera.h:58-64), lens/time draws skipped.
         auto newPath = [&]() {
+            if constexpr (SAMPLE) g = sampleStream(P.seed0, P.seed1, (uint32_t)sample, gpix);
             float u = (fcol + g.uniform()) * P.invW;
             float v = (frow + g.uniform()) * P.invH;
             o = P.cam.pos;
@@ -458,8 +464,18 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
             depthLeft = P.max_depth;
             paths++;
         };
+        // sample mode: close summation block `b` after its last sample
+        auto flush = [&]() {
+            if constexpr (SAMPLE) {
+                if (sample % P.block == 0 || sample == P.spp) {
+                    float* pp = P.partial + 3 * ((size_t)((sample - 1) / P.block) * ((size_t)P.width * P.nrows) + idx);
+                    pp[0] = sum.x; pp[1] = sum.y; pp[2] = sum.z;
+                    sum = f3(0.0f, 0.0f, 0.0f);
+                }
+            }
+        };
         if (P.max_depth <= 0) {
-            for (; sample < P.spp; sample++) { newPath(); sum = add(sum, sky(d, att)); }
+            while (sample < P.spp) { newPath(); sum = add(sum, sky(d, att)); sample++; flush(); }
         } else if (P.spp > 0) {
             newPath();
             uint32_t* my = stk + lane;
@@ -488,16 +504,20 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
                 }
                 if (done) {
                     sum = add(sum, contrib);
-                    if (++sample == P.spp) break;
+                    ++sample;
+                    flush();
+                    if (sample == P.spp) break;
                     newPath();
                 }
             }
         }
-        float* outp = P.out + 3 * idx;   // main.cu:290-293
-        outp[0] = sqrtf(sum.x * P.invSpp);
-        outp[1] = sqrtf(sum.y * P.invSpp);
-        outp[2] = sqrtf(sum.z * P.invSpp);
-        P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+        if constexpr (!SAMPLE) {
+            float* outp = P.out + 3 * idx;   // main.cu:290-293
+            outp[0] = sqrtf(sum.x * P.invSpp);
+            outp[1] = sqrtf(sum.y * P.invSpp);
+            outp[2] = sqrtf(sum.z * P.invSpp);
+            P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+        }
     }
     if (lane == 0) P.tileCost[tile] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - tStart, 0xffffffffull);
     waveReduceAdd(P.counters + 0, c.rays);
@@ -734,14 +754,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             // ------------------------------------------------------------------ NODE
             sVisits += (uint32_t)nN;
             PT_DIAG_ADD(itN, 1u);
-#ifdef PT_PAD_NODE   // experiment: extra dependent VALU work per NODE iteration
-            if (wantNode) {
-                float x_ = inv.x;
-#pragma unroll
-                for (int i_ = 0; i_ < PT_PAD_NODE; i_++) x_ = x_ * 1.0000001f + 1e-30f;
-                if (x_ == 12345.678f) atomicOr(S.err, 4u);
-            }
-#endif
             if (wantNode) {
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
@@ -787,15 +799,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             bool tested = false, sph = false;
             PT_DIAG_ADD(itL, 1u);
             PT_DIAG_ADD(sPops, (uint32_t)nL);
-#ifdef PT_PAD_LEAF   // experiment: extra dependent VALU work per LEAF iteration
-            if (wantLeaf) {
-                float x_ = inv.x;
-#pragma unroll
-                for (int i_ = 0; i_ < PT_PAD_LEAF; i_++) x_ = x_ * 1.0000001f + 1e-30f;
-                if (x_ == 12345.678f) atomicOr(S.err, 4u);
-            }
-#endif
-            if (wantLeaf) {
+            // Every lane tests all of its queued leaves, in order, in this step (the queue then
+            // is empty and the lane rejoins NODE steps; measured -4 % vs one leaf per step).
+            for (int k_ = 0; k_ < kLeafQ; k_++) {
+                const bool act = qn > 0;
+                if (__ballot(act) == 0) break;
+                tested = false;
+                sph = false;
+            if (act) {
                 const uint32_t ref = qref[0];
                 const float lo = lq[0];
 #pragma unroll
@@ -813,6 +824,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             }
             sTris += (uint32_t)__popcll(__ballot(tested && !sph));
             sSph += (uint32_t)__popcll(__ballot(tested && sph));
+            }
         } else {
             // ------------------------------------------------------------------ SHADE
             bool newRay = false, newSample = false;
@@ -1397,7 +1409,8 @@ int envInt(const char* name, int dflt) {
     const char* v = std::getenv(name);
     if (!v || !*v) return dflt;
     int x = std::atoi(v);
-    return x < 1 ? 1 : (x > 64 ? 64 : x);
+    if (x < 1) return dflt;   // "0": the default
+    return x > 64 ? 64 : x;
 }
 
 int stackFor(int depth) {
@@ -1551,7 +1564,8 @@ void launchRender(const RenderParams& P, hipStream_t st) {
     else if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
         renderKernelWF<S, true><<<P.nwaves, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false><<<P.ntiles, kWave, 0, st>>>(P);
-    else renderKernel<S><<<P.ntiles, kWave, 0, st>>>(P);
+    else if (P.partial) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
+    else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
     switch (stack) {
@@ -1996,9 +2010,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (kernel == PT_KERNEL_WIDE && s->nobj > 1 && !s->wide.p) return fail(PT_ERR_STATE, "wide BVH missing");
     const int rng = opts ? opts->rng : PT_RNG_COMPAT;
     if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
-    if (rng == PT_RNG_SAMPLE && kernel != PT_KERNEL_WAVEFRONT) {
+    if (rng == PT_RNG_SAMPLE && kernel == PT_KERNEL_WIDE) {
         if (opts && opts->kernel != PT_KERNEL_DEFAULT)
-            return fail(PT_ERR_INVALID, "pt_render_ex: sample mode runs on the wavefront kernel");
+            return fail(PT_ERR_INVALID, "pt_render_ex: sample mode runs on the wavefront or simple kernel");
         kernel = PT_KERNEL_WAVEFRONT;
     }
     P.kernel = kernel;
@@ -2011,12 +2025,12 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
     // Defaults swept on C3 (tools/gpu_variants.sh): compat mode is bound by its slowest pixels'
-    // sequential chains, so lanes must not wait long (6 / 12: 1,716 ms vs 1,836 at 8 / 16);
+    // sequential chains, so lanes must not wait long (8 / 12; frame times vary by ±5 %);
     // sample mode is throughput-bound and prefers fuller LEAF / SHADE steps (24 / 32: 1,741 ->
     // 1,326..1,355 ms).
     const bool sampleRng = rng == PT_RNG_SAMPLE;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
-                                                 : envInt("PT_LEAF_BATCH", sampleRng ? 24 : 6);
+                                                 : envInt("PT_LEAF_BATCH", sampleRng ? 24 : 8);
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
                                                    : envInt("PT_SHADE_BATCH", sampleRng ? 32 : 12);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;

@@ -343,10 +343,15 @@ def test_sample_mode_bit_exact(pt, orc, gpu, name, w, h, spp, depth, chunk, monk
         monkeypatch.setenv("PT_LEAF_BATCH", leaf)
         monkeypatch.setenv("PT_SHADE_BATCH", shade)
         p = pt.Preset(name, w, h)
-        rgb, st, ref, rst, _, f = render_sample_both(pt, orc, gpu, p, w, h, spp, depth, 11, chunk)
+        rgb, st, ref, rst, s, f = render_sample_both(pt, orc, gpu, p, w, h, spp, depth, 11, chunk)
         np.testing.assert_array_equal(bits(rgb), bits(ref))
         assert st.rays == rst.rays and st.paths == rst.paths == w * h * spp
         assert st.tri_tests == rst.tri_tests and st.sphere_tests == rst.sphere_tests
+        assert st.node_visits >= rst.node_visits   # speculative traversal
+    # the ray-synchronous kernel: same frame, and exactly the reference's traversal order
+    srgb, sst = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk, kernel=pt.KERNEL_SIMPLE)
+    np.testing.assert_array_equal(bits(srgb), bits(ref))
+    assert sst.node_visits == rst.node_visits and sst.tri_tests == rst.tri_tests
 
 
 def test_sample_mode_stateless_and_stripes(pt, orc, gpu):
@@ -382,8 +387,8 @@ def test_sample_mode_options(pt, gpu):
     f = pt.Film(16, 16, 1, device=gpu)
     with pytest.raises(pt.PtError):
         pt.render(s, f, p.camera, 1, 5, rng=5)
-    with pytest.raises(pt.PtError):   # sample mode runs on the wavefront kernel only
-        pt.render(s, f, p.camera, 1, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_SIMPLE)
+    with pytest.raises(pt.PtError):   # sample mode runs on the wavefront and simple kernels
+        pt.render(s, f, p.camera, 1, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WIDE)
     a, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WAVEFRONT)
     b, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE)
     np.testing.assert_array_equal(bits(a), bits(b))
