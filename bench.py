@@ -73,6 +73,20 @@ def cpu_baseline(preset, budget_s: float = 12.0) -> dict:
                       f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads"}
 
 
+def pmc_traffic(workload: str, spp: int, rng: str):
+    """Per-launch HBM traffic of the render kernel on this exact workload, from the committed
+    rocprofv3 PMC passes (profiles/traffic.json, written by tools/collect_profile.py); None if the
+    profile is for a different configuration."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if t.get("workload") != workload or t.get("spp") != spp or t.get("rng") != rng:
+        return None, None
+    return t["traffic_bytes_per_launch"], t["source"]
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,6 +201,10 @@ def main() -> None:
             ptdist.assemble(gathered, h, w, STRIPE, world)
             torch.cuda.synchronize(dev)
         achieved = (kbytes / 1e9) / (kms / 1e3) if kms > 0 else 0.0
+        rng_desc = (("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
+                     f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
+                    "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)")
+        traffic, traffic_src = pmc_traffic(workload, spp, rng_desc)
         out = {
             "metric": METRIC,
             "value": total_rays / elapsed / 1e6,
@@ -207,7 +225,8 @@ def main() -> None:
                                f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
                               "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
                          "algo_bytes_per_launch": kbytes / args.steps,
                          "algo_bytes_source": "reference-order traversal counts of the same frame "

@@ -1,0 +1,61 @@
+"""Copy a tools/profile.sh run (gpurun_out/<TAG>/) into profiles/<TAG>/ and derive the per-launch
+HBM traffic of the sample-mode render kernel from the PMC passes -> profiles/traffic.json (read by
+bench.py for `roofline.traffic`).
+
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 reports both in KiB; on gfx950
+FETCH_SIZE counts half of the bytes of 128-B requests, MI355X_MICROARCH.md "HBM"), taken from the
+wavefront render launch of `bench.py --steps 1 --warmup 0 --no-compat` (warmup launch 1 is the
+ray-synchronous kernel, launch 2 the timed wavefront kernel).
+
+    python tools/collect_profile.py r01_final
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def render_launches(path, counter):
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    return [(r["Kernel_Name"], float(r["Counter_Value"])) for r in rows if "renderKernel" in r["Kernel_Name"]]
+
+
+def main(tag):
+    src = os.path.join(REPO, "gpurun_out", tag)
+    dst = os.path.join(REPO, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    with open(os.path.join(src, "trace", "run_kernel_trace.csv")) as f, \
+            open(os.path.join(dst, "kernel_trace_render.csv"), "w") as g:
+        lines = f.readlines()
+        g.write(lines[0])
+        g.writelines(l for l in lines[1:] if "render" in l or "reduceChunks" in l)
+    for p in ("fetch", "write", "tcc", "sq"):
+        shutil.copy(os.path.join(src, f"pmc_{p}", "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
+
+    bench = json.loads(open(os.path.join(src, "bench.json")).read())
+    fetch = render_launches(os.path.join(dst, "pmc_fetch.csv"), "FETCH_SIZE")
+    write = render_launches(os.path.join(dst, "pmc_write.csv"), "WRITE_SIZE")
+    wf_fetch = [v for k, v in fetch if "renderKernelWF" in k] or [fetch[-1][1]]
+    wf_write = [v for k, v in write if "renderKernelWF" in k] or [write[-1][1]]
+    fetch_b = 2.0 * wf_fetch[-1] * 1024.0
+    write_b = wf_write[-1] * 1024.0
+    cfg = bench["config"]
+    out = {
+        "workload": cfg["workload"], "spp": cfg["spp"], "rng": cfg["rng"],
+        "traffic_bytes_per_launch": fetch_b + write_b,
+        "fetch_bytes": fetch_b, "write_bytes": write_b,
+        "source": f"profiles/{tag}/pmc_fetch.csv + pmc_write.csv (separate rocprofv3 --pmc passes; "
+                  "2 x FETCH_SIZE + WRITE_SIZE, KiB -> B)",
+    }
+    with open(os.path.join(REPO, "profiles", "traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
