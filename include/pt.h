@@ -110,6 +110,9 @@ int pt_morton_keys(const pt_object* objs, int64_t n, int include_origin, uint64_
 int pt_write_png(const char* path, const float* rgb, int width, int height);
 /* Quantise exactly like saveColor: (uint8)(clamp(c, 0, 0.999) * 256), alpha 255, row flip. */
 int pt_quantize_rgba8(const float* rgb, int width, int height, uint8_t* rgba);
+/* PngImage::write of an already quantised frame (pt_render_ex with PT_OUT_RGBA8): rgba is
+ * row-major with row 0 = bottom, flipped on output like pt_write_png. */
+int pt_write_png_rgba8(const char* path, const uint8_t* rgba, int width, int height);
 
 /* ---------------------------------------------------------------- device (MI355X, gfx950) */
 /* Replaces the scene upload of generate*WorldOnHost (main.cu:173-192: cudaMalloc/cudaMemcpy,
@@ -159,19 +162,36 @@ int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int
  *   random numbers; does not advance the film's XORWOW streams.  Needs chunk-count x pixels
  *   x 12 bytes of device memory for the block sums.
  * leaf_batch / shade_batch: wavefront thresholds in lanes (0 = default).
- * flags: PT_RENDER_IDENTITY_ORDER disables the longest-tile-first launch order. */
+ * flags: PT_RENDER_IDENTITY_ORDER disables the longest-tile-first launch order;
+ *   PT_RENDER_ACCUMULATE adds the frame to the film's running sums (progressive rendering,
+ *   the headless counterpart of the reference's interactive loop renderToGL/renderBySurface,
+ *   main.cu:307-340, 489-528) and outputs sqrt(all accumulated samples' sum / their count);
+ *   compat mode continues the film's XORWOW streams, sample mode continues the sample index.
+ *   pt_film_clear() restarts the accumulation (e.g. after pt_camera_move).  At most 2^24 - 1
+ *   accumulated samples per pixel.
+ * out_format: PT_OUT_RGB32F (3 floats per pixel), PT_OUT_RGBA8 (4 bytes per pixel, quantised on
+ *   the device exactly like PngImage::saveColor, png_image.h:24-30: (uint8)(clamp(c,0,0.999)*256),
+ *   alpha 255; rows in film order, row 0 = bottom, pt_write_png_rgba8 flips them) or
+ *   PT_OUT_RGBA8_SURFACE (renderBySurface's conversion, main.cu:327-331: (unsigned)(c*255) in an
+ *   8-bit field).  For the 8-bit formats `out_rgb` points to n_pixels x 4 bytes. */
 enum { PT_KERNEL_DEFAULT = 0, PT_KERNEL_SIMPLE = 1, PT_KERNEL_WAVEFRONT = 2, PT_KERNEL_WIDE = 3 };
 enum { PT_RNG_COMPAT = 0, PT_RNG_SAMPLE = 1 };
+enum { PT_OUT_RGB32F = 0, PT_OUT_RGBA8 = 1, PT_OUT_RGBA8_SURFACE = 2 };
 #define PT_RENDER_IDENTITY_ORDER 1
+#define PT_RENDER_ACCUMULATE 2
 typedef struct {
     int32_t kernel, leaf_batch, shade_batch, flags;
-    int32_t rng, chunk, reserved0, reserved1;
+    int32_t rng, chunk, out_format, reserved1;
 } pt_render_opts;
 int pt_render_ex(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
                  float* out_rgb, int out_on_device, void* stream, const pt_render_opts* opts,
                  pt_stats* stats);
 /* Re-initialise the film's streams to their initRandom state (asynchronous on `stream`). */
 int pt_film_reset(pt_film* film, void* stream);
+/* Progressive rendering: zero the film's accumulated sums (asynchronous on `stream`); the number
+ * of samples per pixel accumulated so far. */
+int pt_film_clear(pt_film* film, void* stream);
+int pt_film_accumulated(pt_film* film, int64_t* samples);
 void pt_film_destroy(pt_film* film);
 void pt_scene_destroy(pt_scene* scene);   /* replaces clearWorldStates (main.cu:451-460) */
 

@@ -57,6 +57,10 @@ for name, res, args in [
                               C.c_int, _P, _P, C.POINTER(Stats), C.c_int, _P]),
     ("orc_render_sample", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
                                     C.c_int, C.c_uint64, C.c_int, _P, C.POINTER(Stats), C.c_int]),
+    ("orc_render3", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
+                              C.c_int, _P, _P, C.POINTER(Stats), C.c_int, _P, _P]),
+    ("orc_render_sample2", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
+                                     C.c_int, C.c_uint64, C.c_int, _P, C.POINTER(Stats), C.c_int, C.c_uint32, _P]),
     ("orc_philox_word", C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int]),
     ("orc_sample_stream", None, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_void_p]),
     ("orc_render", C.c_int, [_P, C.c_int64, _P, C.c_int64, _P, _P, C.c_int, C.c_int, _P, C.c_int, C.c_int,
@@ -178,6 +182,71 @@ def render_sample(objects, materials, nodes, camera, width, height, rows, spp, m
                           width, height, _ptr(rows), len(rows), spp, max_depth, seed, chunk, _ptr(out), C.byref(st),
                           nthreads)
     return out, st
+
+
+def render_sums(objects, materials, nodes, camera, width, height, rows, spp, max_depth, states, nthreads=1):
+    """orc_render + the raw per-pixel sample sums: (rgb, sums float32 (npix, 3), Stats)."""
+    objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+    materials = np.ascontiguousarray(materials, MATERIAL_DTYPE)
+    rows = np.ascontiguousarray(rows, np.int32)
+    camera = np.ascontiguousarray(camera, np.float32)
+    assert states.dtype == np.uint32 and states.flags["C_CONTIGUOUS"] and states.shape == (len(rows) * width, 6)
+    out = np.zeros((len(rows) * width, 3), np.float32)
+    sums = np.zeros((len(rows) * width, 3), np.float32)
+    st = Stats()
+    lib.orc_render3(_ptr(objects), len(objects), _ptr(materials), len(materials), _ptr(nodes), _ptr(camera), width,
+                    height, _ptr(rows), len(rows), spp, max_depth, _ptr(states), _ptr(out), C.byref(st), nthreads,
+                    None, _ptr(sums))
+    return out, sums, st
+
+
+def render_sample_sums(objects, materials, nodes, camera, width, height, rows, spp, max_depth, seed, chunk,
+                       sample_base=0, nthreads=1):
+    """Sample mode with samples numbered from sample_base: (rgb, sums float32 (npix, 3), Stats)."""
+    objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+    materials = np.ascontiguousarray(materials, MATERIAL_DTYPE)
+    rows = np.ascontiguousarray(rows, np.int32)
+    camera = np.ascontiguousarray(camera, np.float32)
+    out = np.zeros((len(rows) * width, 3), np.float32)
+    sums = np.zeros((len(rows) * width, 3), np.float32)
+    st = Stats()
+    lib.orc_render_sample2(_ptr(objects), len(objects), _ptr(materials), len(materials), _ptr(nodes), _ptr(camera),
+                           width, height, _ptr(rows), len(rows), spp, max_depth, seed, chunk, _ptr(out), C.byref(st),
+                           nthreads, sample_base, _ptr(sums))
+    return out, sums, st
+
+
+def accumulate(frame_sums, frame_spps):
+    """Progressive resolve (pt_render_ex with PT_RENDER_ACCUMULATE after each frame): the running
+    fp32 sum A_k = A_{k-1} + S_k (A_0 = 0) and the image sqrt(A_k * (1 / samples so far)), in
+    float32 arithmetic.  Returns the list of images, one per frame."""
+    a = np.zeros_like(np.asarray(frame_sums[0], np.float32))
+    n, out = 0, []
+    for s, spp in zip(frame_sums, frame_spps):
+        a = (a + np.asarray(s, np.float32)).astype(np.float32)
+        n += spp
+        out.append(np.sqrt((a * (np.float32(1.0) / np.float32(n))).astype(np.float32)).astype(np.float32))
+    return out
+
+
+def quantize_png(rgb):
+    """PngImage::saveColor (png_image.h:24-30): (uint8)(clamp(c, 0, 0.999f) * 256), alpha 255;
+    rows kept in film order.  (npix, 3) float32 -> (npix, 4) uint8."""
+    c = np.asarray(rgb, np.float32)
+    c = np.where(c < 0, np.float32(0), np.where(c > np.float32(0.999), np.float32(0.999), c)).astype(np.float32)
+    q = np.full((c.shape[0], 4), 255, np.uint8)
+    q[:, :3] = (c * np.float32(256.0)).astype(np.float32).astype(np.uint8)
+    return q
+
+
+def quantize_surface(rgb):
+    """renderBySurface (main.cu:327-331): (unsigned)(c * 255) stored in an 8-bit field, alpha 255.
+    (A negative value -- never produced by the path -- converts to 0, as v_cvt_u32_f32 does.)"""
+    c = np.asarray(rgb, np.float32)
+    q = np.full((c.shape[0], 4), 255, np.uint8)
+    x = np.maximum((c * np.float32(255.0)).astype(np.float32), np.float32(0))
+    q[:, :3] = (x.astype(np.uint32) & 0xFF).astype(np.uint8)
+    return q
 
 
 def render_pixel_rays(objects, materials, nodes, camera, width, height, rows, spp, max_depth, states, nthreads=1):

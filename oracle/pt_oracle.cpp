@@ -666,6 +666,14 @@ extern "C" {
 int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
                 const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
                 uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays) {
+    return orc_render3(objs, nobj, mats, nmat, nodes, cam, width, height, rows, nrows, spp, max_depth, states, out_rgb,
+                       stats, nthreads, pixel_rays, nullptr);
+}
+
+int orc_render3(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat, const orc_node* nodes,
+                const orc_camera* cam, int width, int height, const int32_t* rows, int nrows, int spp, int max_depth,
+                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays,
+                float* out_sum) {
     (void)nmat; (void)height;
     if (nthreads < 1) nthreads = 1;
     const V3 pos = load3(cam->origin), ll = load3(cam->lower_left);
@@ -717,6 +725,7 @@ int orc_render2(const orc_object* objs, int64_t nobj, const orc_material* mats, 
                     sum = sum + c;                                                      // vec3::operator+=
                 }
                 if (pixel_rays) pixel_rays[k] = (uint32_t)(local.rays - rays0);
+                if (out_sum) { out_sum[3 * k + 0] = sum.x; out_sum[3 * k + 1] = sum.y; out_sum[3 * k + 2] = sum.z; }
                 out_rgb[3 * k + 0] = std::sqrt(sum.x * invSpp);                        // main.cu:290-293
                 out_rgb[3 * k + 1] = std::sqrt(sum.y * invSpp);
                 out_rgb[3 * k + 2] = std::sqrt(sum.z * invSpp);
@@ -744,6 +753,14 @@ int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* 
                       const orc_node* nodes, const orc_camera* cam, int width, int height, const int32_t* rows,
                       int nrows, int spp, int max_depth, uint64_t seed, int chunk, float* out_rgb, orc_stats* stats,
                       int nthreads) {
+    return orc_render_sample2(objs, nobj, mats, nmat, nodes, cam, width, height, rows, nrows, spp, max_depth, seed,
+                              chunk, out_rgb, stats, nthreads, 0, nullptr);
+}
+
+int orc_render_sample2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
+                       const orc_node* nodes, const orc_camera* cam, int width, int height, const int32_t* rows,
+                       int nrows, int spp, int max_depth, uint64_t seed, int chunk, float* out_rgb, orc_stats* stats,
+                       int nthreads, uint32_t sample_base, float* out_sum) {
     (void)nmat;
     if (nthreads < 1) nthreads = 1;
     if (chunk < 1) chunk = 1;
@@ -763,13 +780,14 @@ int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* 
                     V3 part{0, 0, 0};
                     for (int s = c0; s < std::min(spp, c0 + chunk); s++) {
                         uint32_t st[6];
-                        sampleStream(seed, (uint32_t)s, pixel, st);
+                        sampleStream(seed, sample_base + (uint32_t)s, pixel, st);
                         XorwowRng rng{st};
                         part = part + tracePath(objs, nobj, mats, nodes, cam, col, row, invW, invH, max_depth, rng, local);
                     }
                     total = total + part;
                 }
                 const int64_t k = (int64_t)ri * width + col;
+                if (out_sum) { out_sum[3 * k + 0] = total.x; out_sum[3 * k + 1] = total.y; out_sum[3 * k + 2] = total.z; }
                 out_rgb[3 * k + 0] = std::sqrt(total.x * invSpp);
                 out_rgb[3 * k + 1] = std::sqrt(total.y * invSpp);
                 out_rgb[3 * k + 2] = std::sqrt(total.z * invSpp);

@@ -84,6 +84,21 @@ int orc_render_sample(const orc_object* objs, int64_t nobj, const orc_material* 
                       const orc_node* nodes, const orc_camera* cam, int width, int height,
                       const int32_t* rows, int nrows, int spp, int max_depth, uint64_t seed, int chunk,
                       float* out_rgb, orc_stats* stats, int nthreads);
+
+/* orc_render2 that also writes the raw per-pixel sample sums (before sqrt(sum / spp)) to
+ * out_sum (3 floats per pixel) when non-null: the input of progressive accumulation. */
+int orc_render3(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
+                const orc_node* nodes, const orc_camera* cam, int width, int height,
+                const int32_t* rows, int nrows, int spp, int max_depth,
+                uint32_t* states, float* out_rgb, orc_stats* stats, int nthreads, uint32_t* pixel_rays,
+                float* out_sum);
+
+/* orc_render_sample whose samples are numbered from sample_base (a progressive frame continues
+ * the sample sequence), plus the raw per-pixel sums (chunk sums added in order) when out_sum. */
+int orc_render_sample2(const orc_object* objs, int64_t nobj, const orc_material* mats, int64_t nmat,
+                       const orc_node* nodes, const orc_camera* cam, int width, int height,
+                       const int32_t* rows, int nrows, int spp, int max_depth, uint64_t seed, int chunk,
+                       float* out_rgb, orc_stats* stats, int nthreads, uint32_t sample_base, float* out_sum);
 uint32_t orc_philox_word(uint64_t key, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, int word);
 void orc_sample_stream(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_t state[6]);  /* {d, v0..v4} */
 

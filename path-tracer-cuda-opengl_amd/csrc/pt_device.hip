@@ -406,7 +406,22 @@ struct RenderParams {
     uint32_t ntasks;                          // tile slots x nblocks x 64
     int nwaves;                               // persistent waves launched
     uint32_t seed0, seed1;
+    uint32_t sampleBase;                      // sample mode: index of the frame's first sample
+    int rawOut;                               // compat: store the raw sample sum (resolveKernel follows)
 };
+
+// Compat mode end of a pixel: sqrt(sum / spp) (main.cu:290-293), or the raw sum when a resolve
+// pass (accumulation / 8-bit output) follows.
+__device__ __forceinline__ void storePixel(const RenderParams& P, size_t idx, float3 sum) {
+    float* outp = P.out + 3 * idx;
+    if (P.rawOut) {
+        outp[0] = sum.x; outp[1] = sum.y; outp[2] = sum.z;
+    } else {
+        outp[0] = sqrtf(sum.x * P.invSpp);
+        outp[1] = sqrtf(sum.y * P.invSpp);
+        outp[2] = sqrtf(sum.z * P.invSpp);
+    }
+}
 
 __device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
     return ((lrow / sh) * nparts + part) * sh + lrow % sh;
@@ -455,7 +470,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
         int depthLeft = 0, sample = 0;
         // newPath: main.cu:284-286 + camera::get_ray (camera.h:58-64), lens/time draws skipped.
         auto newPath = [&]() {
-            if constexpr (SAMPLE) g = sampleStream(P.seed0, P.seed1, (uint32_t)sample, gpix);
+            if constexpr (SAMPLE) g = sampleStream(P.seed0, P.seed1, P.sampleBase + (uint32_t)sample, gpix);
             float u = (fcol + g.uniform()) * P.invW;
             float v = (frow + g.uniform()) * P.invH;
             o = P.cam.pos;
@@ -512,10 +527,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
             }
         }
         if constexpr (!SAMPLE) {
-            float* outp = P.out + 3 * idx;   // main.cu:290-293
-            outp[0] = sqrtf(sum.x * P.invSpp);
-            outp[1] = sqrtf(sum.y * P.invSpp);
-            outp[2] = sqrtf(sum.z * P.invSpp);
+            storePixel(P, idx, sum);
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
         }
     }
@@ -688,7 +700,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     do {                                                                                          \
         if constexpr (SAMPLE) {                                                                   \
             fcol = (float)(cr & 0xffffu);                                                         \
-            g = sampleStream(P.seed0, P.seed1, (uint32_t)sample,                                  \
+            g = sampleStream(P.seed0, P.seed1, P.sampleBase + (uint32_t)sample,                   \
                              (uint32_t)frow * (uint32_t)P.width + (cr & 0xffffu));                \
         }                                                                                         \
         const float u_ = (fcol + g.uniform()) * P.invW;                                           \
@@ -876,10 +888,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     }
     if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
         if (valid) {
-            float* outp = P.out + 3 * idx;   // main.cu:290-293
-            outp[0] = sqrtf(sum.x * P.invSpp);
-            outp[1] = sqrtf(sum.y * P.invSpp);
-            outp[2] = sqrtf(sum.z * P.invSpp);
+            storePixel(P, idx, sum);
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
         }
     }
@@ -915,21 +924,55 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
 #undef PT_FINISH_TASK
 #undef PT_DIAG_ADD
 
-// Sample mode epilogue: out = sqrt(sum over blocks (in order) of the block sums / spp).
-__global__ __launch_bounds__(256) void reduceChunksKernel(const float* __restrict__ partial, float* out, int64_t npix,
-                                                          int nchunks, float invSpp) {
+// Frame epilogue (one lane per pixel).  The frame's linear sum S is the raw compat sum
+// (`nblocks` = 0) or, in sample mode, the block sums added in order.  Accumulating films keep
+// A += S over frames (progressive rendering, the headless counterpart of the reference's
+// interactive loop, main.cu:489-528) and resolve sqrt(A * (1 / samples so far)); otherwise
+// sqrt(S * (1 / spp)) (main.cu:290-293).  Output: fp32 RGB, or 8-bit RGBA quantised like
+// PngImage::saveColor (png_image.h:24-30: (uint8)(clamp(c, 0, 0.999) * 256), alpha 255) or like
+// renderBySurface (main.cu:327-331: (unsigned)(c * 255) into an 8-bit field, alpha 255).
+// Rows stay in film order (row 0 = bottom); the PNG writer flips them.
+__global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ src, int nblocks, float* accum,
+                                                     float inv, int format, void* out, int64_t npix) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix) return;
-    float x = 0.0f, y = 0.0f, z = 0.0f;
-    for (int c = 0; c < nchunks; c++) {
-        const float* q = partial + 3 * ((size_t)c * (size_t)npix + (size_t)i);
-        x = x + q[0];
-        y = y + q[1];
-        z = z + q[2];
+    float x, y, z;
+    if (nblocks == 0) {
+        x = src[3 * i + 0]; y = src[3 * i + 1]; z = src[3 * i + 2];
+    } else {
+        x = 0.0f; y = 0.0f; z = 0.0f;
+        for (int c = 0; c < nblocks; c++) {
+            const float* q = src + 3 * ((size_t)c * (size_t)npix + (size_t)i);
+            x = x + q[0];
+            y = y + q[1];
+            z = z + q[2];
+        }
     }
-    out[3 * i + 0] = sqrtf(x * invSpp);
-    out[3 * i + 1] = sqrtf(y * invSpp);
-    out[3 * i + 2] = sqrtf(z * invSpp);
+    if (accum) {
+        float* a = accum + 3 * i;
+        x = a[0] + x; y = a[1] + y; z = a[2] + z;
+        a[0] = x; a[1] = y; a[2] = z;
+    }
+    const float c[3] = {sqrtf(x * inv), sqrtf(y * inv), sqrtf(z * inv)};
+    if (format == PT_OUT_RGB32F) {
+        float* o = static_cast<float*>(out) + 3 * i;
+        o[0] = c[0]; o[1] = c[1]; o[2] = c[2];
+        return;
+    }
+    uint32_t px = 0xff000000u;
+    for (int k = 0; k < 3; k++) {
+        uint32_t b;
+        if (format == PT_OUT_RGBA8) {
+            float v = c[k];                  // utility.h:40-44 clamp(x, 0, 0.999f), then * 256
+            if (v < 0.0f) v = 0.0f;
+            if (v > 0.999f) v = 0.999f;
+            b = (uint32_t)(v * 256.0f);
+        } else {
+            b = (uint32_t)(c[k] * 255.0f) & 0xffu;
+        }
+        px |= b << (8 * k);
+    }
+    static_cast<uint32_t*>(out)[i] = px;
 }
 
 // 4-wide variant of renderKernelWF.  Wide node (128 B = 8 x float4): SoA child boxes
@@ -1164,10 +1207,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         }
     }
     if (valid) {
-        float* outp = P.out + 3 * idx;   // main.cu:290-293
-        outp[0] = sqrtf(sum.x * P.invSpp);
-        outp[1] = sqrtf(sum.y * P.invSpp);
-        outp[2] = sqrtf(sum.z * P.invSpp);
+        storePixel(P, idx, sum);
         P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
     }
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
@@ -1457,6 +1497,9 @@ struct pt_film {
     int costSpp = 0;
     DevBuf partial, taskCounter;  // sample mode: per-block partial sums; task counter
     size_t partialBytes = 0;
+    DevBuf sums;                  // compat mode: raw per-pixel sample sums of the frame (resolve input)
+    DevBuf accum;                 // progressive rendering: fp32 RGB running sums of every accumulated frame
+    int64_t accumSamples = 0;     // samples per pixel in `accum`
     int cus = 0;                  // compute units of the device (persistent grid size)
 };
 
@@ -1912,6 +1955,21 @@ int pt_film_reset(pt_film* f, void* stream) {
     return filmInit(f, (hipStream_t)stream);
 }
 
+int pt_film_clear(pt_film* f, void* stream) {
+    if (!f) return fail(PT_ERR_INVALID, "pt_film_clear: null film");
+    int rc = setDevice(f->device);
+    if (rc) return rc;
+    if (f->accum.p) HIP_TRY(hipMemsetAsync(f->accum.p, 0, (size_t)std::max<int64_t>(1, f->npix) * 12, (hipStream_t)stream));
+    f->accumSamples = 0;
+    return PT_OK;
+}
+
+int pt_film_accumulated(pt_film* f, int64_t* samples) {
+    if (!f || !samples) return fail(PT_ERR_INVALID, "pt_film_accumulated: null argument");
+    *samples = f->accumSamples;
+    return PT_OK;
+}
+
 int pt_film_info(pt_film* f, int* nrows, int64_t* npix) {
     if (!f) return fail(PT_ERR_INVALID, "pt_film_info: null film");
     if (nrows) *nrows = f->nrows;
@@ -1968,11 +2026,18 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (rc) return rc;
     hipStream_t st = on_dev ? (hipStream_t)stream : 0;
     const int64_t np = f->npix;
+    const int fmt = opts ? opts->out_format : PT_OUT_RGB32F;
+    if (fmt != PT_OUT_RGB32F && fmt != PT_OUT_RGBA8 && fmt != PT_OUT_RGBA8_SURFACE)
+        return fail(PT_ERR_INVALID, "pt_render_ex: unknown output format");
+    const bool accumulate = opts && (opts->flags & PT_RENDER_ACCUMULATE);
+    const size_t outBpp = fmt == PT_OUT_RGB32F ? 12 : 4;
+    if (accumulate && f->accumSamples + spp >= (1ll << 24))
+        return fail(PT_ERR_INVALID, "pt_render_ex: accumulated samples must stay below 2^24");
     DevBuf dout;
-    float* dst = out;
+    void* dst = out;
     if (!on_dev) {
-        if ((rc = devAlloc(dout, (size_t)std::max<int64_t>(1, np) * 12))) return rc;
-        dst = dout.as<float>();
+        if ((rc = devAlloc(dout, (size_t)std::max<int64_t>(1, np) * outBpp))) return rc;
+        dst = dout.p;
     }
     HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16 * sizeof(unsigned long long), st));
     RenderParams P;
@@ -1983,7 +2048,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.cam.ver = make_float3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
     uint32_t* b = f->state.as<uint32_t>();
     P.sd = b; P.s0 = b + np; P.s1 = b + 2 * np; P.s2 = b + 3 * np; P.s3 = b + 4 * np; P.s4 = b + 5 * np;
-    P.out = dst;
+    P.out = static_cast<float*>(dst);
+    P.rawOut = 0;
+    P.sampleBase = 0;
     P.counters = s->counters.as<unsigned long long>();
     P.width = f->width;
     P.nrows = f->nrows;
@@ -2070,6 +2137,22 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
     }
+    // A resolve pass follows the render kernel in sample mode (block sums) and whenever the film
+    // accumulates or the output is 8-bit; compat kernels then store raw sums into f->sums.
+    const bool resolve = np > 0 && (sample || accumulate || fmt != PT_OUT_RGB32F);
+    if (resolve && !sample) {
+        if (!f->sums.p && (rc = devAlloc(f->sums, (size_t)np * 12))) return rc;
+        P.out = f->sums.as<float>();
+        P.rawOut = 1;
+    }
+    if (accumulate) {
+        if (!f->accum.p) {
+            if ((rc = devAlloc(f->accum, (size_t)std::max<int64_t>(1, np) * 12))) return rc;
+            HIP_TRY(hipMemsetAsync(f->accum.p, 0, (size_t)std::max<int64_t>(1, np) * 12, st));
+            f->accumSamples = 0;
+        }
+        if (sample) P.sampleBase = (uint32_t)f->accumSamples;   // frames continue the sample sequence
+    }
     P.tileCost = f->tileCost.as<unsigned>();
     P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
     P.prioTiles = (P.tileOrder && !sample) ? envInt("PT_PRIO_TILES", 1024) : 0;
@@ -2090,10 +2173,15 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
         return rc;
     }
-    if (sample) {
-        reduceChunksKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(P.partial, dst, np, P.nblocks, P.invSpp);
+    if (resolve) {
+        const float inv = accumulate ? 1.0f / (float)(f->accumSamples + spp) : P.invSpp;
+        resolveKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(sample ? P.partial : f->sums.as<float>(),
+                                                                     sample ? P.nblocks : 0,
+                                                                     accumulate ? f->accum.as<float>() : nullptr,
+                                                                     inv, fmt, dst, np);
         HIP_TRY(hipGetLastError());
     }
+    if (accumulate) f->accumSamples += spp;
     HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));
     float ms = 0;
@@ -2119,7 +2207,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
             std::fclose(fp);
         }
     }
-    if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * 12, hipMemcpyDeviceToHost));
+    if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * outBpp, hipMemcpyDeviceToHost));
     unsigned long long c[16] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     fillStats(stats, c, ms);

@@ -540,4 +540,14 @@ int pt_write_png(const char* path, const float* rgb, int w, int h) {
     return PT_OK;
 }
 
+int pt_write_png_rgba8(const char* path, const uint8_t* rgba, int w, int h) {
+    if (!path || !rgba || w <= 0 || h <= 0) return fail(PT_ERR_INVALID, "pt_write_png_rgba8: bad argument");
+    PngImage png(w, h);
+    const size_t stride = (size_t)w * 4;
+    for (int row = 0; row < h; row++)   // row flip of main.cu:481
+        std::memcpy(png.pixels() + (size_t)(h - row - 1) * stride, rgba + (size_t)row * stride, stride);
+    if (!png.write(path)) return fail(PT_ERR_IO, std::string("pt_write_png_rgba8: cannot write ") + path);
+    return PT_OK;
+}
+
 }  // extern "C"

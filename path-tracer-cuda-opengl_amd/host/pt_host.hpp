@@ -79,6 +79,7 @@ public:
     int channel() const { return mDataN; }
     bool write(const char* filename) const;
     const std::vector<uint8_t>& data() const { return mData; }
+    uint8_t* pixels() { return mData.data(); }   // raw RGBA8 rows, top row first (as written)
 
 private:
     std::vector<uint8_t> mData;

@@ -52,11 +52,12 @@ class Stats(C.Structure):
 
 class RenderOpts(C.Structure):
     _fields_ = [("kernel", C.c_int32), ("leaf_batch", C.c_int32), ("shade_batch", C.c_int32), ("flags", C.c_int32),
-                ("rng", C.c_int32), ("chunk", C.c_int32), ("reserved0", C.c_int32), ("reserved1", C.c_int32)]
+                ("rng", C.c_int32), ("chunk", C.c_int32), ("out_format", C.c_int32), ("reserved1", C.c_int32)]
 
 
 RNG_COMPAT, RNG_SAMPLE = 0, 1
-IDENTITY_ORDER = 1
+IDENTITY_ORDER, ACCUMULATE = 1, 2
+OUT_RGB32F, OUT_RGBA8, OUT_RGBA8_SURFACE = 0, 1, 2
 
 
 KERNEL_DEFAULT, KERNEL_SIMPLE, KERNEL_WAVEFRONT, KERNEL_WIDE = 0, 1, 2, 3
@@ -75,6 +76,7 @@ EXPORTS = [
     "pt_quantize_rgba8", "pt_scene_create", "pt_scene_build_bvh", "pt_scene_bvh_info", "pt_scene_download_bvh",
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
+    "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -111,6 +113,9 @@ _sig = {
     "pt_render_ex": (C.c_int, [_P, _P, C.POINTER(Camera), C.c_int, C.c_int, _P, C.c_int, _P, C.POINTER(RenderOpts),
                                C.POINTER(Stats)]),
     "pt_film_reset": (C.c_int, [_P, _P]),
+    "pt_film_clear": (C.c_int, [_P, _P]),
+    "pt_film_accumulated": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "pt_write_png_rgba8": (C.c_int, [C.c_char_p, _P, C.c_int, C.c_int]),
     "pt_film_destroy": (None, [_P]),
     "pt_scene_destroy": (None, [_P]),
 }
@@ -149,6 +154,11 @@ def camera_make(frm, at, vfov, aspect, aperture=0.0, focus=10.0, t0=0.0, t1=1.0)
     a = np.asarray(at, np.float32)
     _check(lib.pt_camera_make(_ptr(f), _ptr(a), vfov, aspect, aperture, focus, t0, t1, C.byref(cam)), "pt_camera_make")
     return cam
+
+
+def camera_move(cam: Camera, direction: int, delta_time: float) -> None:
+    """camera::processKeyboard (camera.h:41-56): 0 FORWARD 1 BACKWARD 2 LEFT 3 RIGHT 4 UP 5 DOWN."""
+    _check(lib.pt_camera_move(C.byref(cam), direction, delta_time), "pt_camera_move")
 
 
 def camera_to_array(cam: Camera) -> np.ndarray:
@@ -198,6 +208,13 @@ def quantize_rgba8(rgb: np.ndarray, width: int, height: int) -> np.ndarray:
     out = np.zeros((height, width, 4), np.uint8)
     _check(lib.pt_quantize_rgba8(_ptr(rgb), width, height, _ptr(out)), "pt_quantize_rgba8")
     return out
+
+
+def write_png_rgba8(path: str, rgba: np.ndarray, width: int, height: int) -> None:
+    """PNG of a device-quantised frame (OUT_RGBA8 rows, row 0 = bottom; flipped on output)."""
+    rgba = np.ascontiguousarray(rgba, np.uint8)
+    assert rgba.size == width * height * 4
+    _check(lib.pt_write_png_rgba8(path.encode(), _ptr(rgba), width, height), "pt_write_png_rgba8")
 
 
 def write_png(path: str, rgb: np.ndarray, width: int, height: int) -> None:
@@ -287,6 +304,16 @@ class Film:
         """Back to the initRandom state: curand_init(seed, pixel, 0) for every pixel."""
         _check(lib.pt_film_reset(self.h, C.c_void_p(int(stream) if stream else 0)), "pt_film_reset")
 
+    def clear(self, stream=None) -> None:
+        """Progressive rendering: restart the accumulation (e.g. after the camera moved)."""
+        _check(lib.pt_film_clear(self.h, C.c_void_p(int(stream) if stream else 0)), "pt_film_clear")
+
+    @property
+    def accumulated(self) -> int:
+        n = C.c_int64()
+        _check(lib.pt_film_accumulated(self.h, C.byref(n)), "pt_film_accumulated")
+        return n.value
+
     def close(self) -> None:
         if self.h:
             lib.pt_film_destroy(self.h)
@@ -301,14 +328,23 @@ class Film:
 
 def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, out=None, stream=None,
            kernel: int = KERNEL_DEFAULT, leaf_batch: int = 0, shade_batch: int = 0, rng: int = RNG_COMPAT,
-           chunk: int = 0, flags: int = 0):
+           chunk: int = 0, flags: int = 0, accumulate: bool = False, out_format: int = OUT_RGB32F):
     """Render spp samples per pixel of the film's rows.  `out` may be a numpy array (host) or
     an integer device pointer (then `stream` is a hipStream_t handle or None).  Returns
-    (rgb or None, Stats)."""
+    (rgb or None, Stats); rgb is float32 (n_pixels, 3), or uint8 (n_pixels, 4) for the 8-bit
+    output formats.  accumulate=True adds the frame to the film's running sums (progressive)."""
     st = Stats()
-    opts = RenderOpts(kernel, leaf_batch, shade_batch, flags, rng, chunk, 0, 0)
+    if accumulate:
+        flags |= ACCUMULATE
+    opts = RenderOpts(kernel, leaf_batch, shade_batch, flags, rng, chunk, out_format, 0)
     if out is None or isinstance(out, np.ndarray):
-        rgb = out if out is not None else np.zeros((film.n_pixels, 3), np.float32)
+        if out is None:
+            rgb = (np.zeros((film.n_pixels, 3), np.float32) if out_format == OUT_RGB32F
+                   else np.zeros((film.n_pixels, 4), np.uint8))
+        else:
+            rgb = out
+            want = (np.float32, 3) if out_format == OUT_RGB32F else (np.uint8, 4)
+            assert rgb.dtype == want[0] and rgb.flags["C_CONTIGUOUS"] and rgb.size >= film.n_pixels * want[1]
         _check(lib.pt_render_ex(scene.h, film.h, C.byref(camera), spp, max_depth, _ptr(rgb), 0, None, C.byref(opts),
                                 C.byref(st)), "pt_render_ex")
         return rgb, st

@@ -132,6 +132,34 @@ def test_write_png_roundtrip(pt, tmp_path):
     np.testing.assert_array_equal(_read_png(path), pt.quantize_rgba8(rgb, w, h))
 
 
+def test_write_png_rgba8_matches_write_png(pt, orc, tmp_path):
+    """A frame quantised on the device (PT_OUT_RGBA8: saveColor per pixel, rows bottom-up) and
+    written with pt_write_png_rgba8 gives the same file as pt_write_png of the fp32 frame."""
+    w, h = 9, 5
+    rgb = np.random.default_rng(1).uniform(-0.1, 1.1, (w * h, 3)).astype(np.float32)
+    a, b = str(tmp_path / "a.png"), str(tmp_path / "b.png")
+    pt.write_png(a, rgb, w, h)
+    pt.write_png_rgba8(b, orc.quantize_png(rgb), w, h)
+    assert open(a, "rb").read() == open(b, "rb").read()
+
+
+def test_quantisers_restate_reference_formulas(orc):
+    c = np.float32([[-0.5, 0.0, 0.5], [0.999, 0.9995, 1.0], [1.7, 0.00390625, 0.99609375]])
+    q = orc.quantize_png(c)
+    np.testing.assert_array_equal(q[:, :3], [[0, 0, 128], [255, 255, 255], [255, 1, 255]])
+    s = orc.quantize_surface(c)
+    np.testing.assert_array_equal(s[:, :3], [[0, 0, 127], [254, 254, 255], [177, 0, 254]])
+    assert (q[:, 3] == 255).all() and (s[:, 3] == 255).all()
+
+
+def test_oracle_accumulate_restatement(orc):
+    s1 = np.float32([[1.0, 2.0, 0.5]])
+    s2 = np.float32([[3.0, 0.0, 0.25]])
+    imgs = orc.accumulate([s1, s2], [2, 2])
+    np.testing.assert_array_equal(imgs[0], np.sqrt(s1 * np.float32(0.5)))
+    np.testing.assert_array_equal(imgs[1], np.sqrt((s1 + s2) * np.float32(0.25)))
+
+
 def test_device_calls_fail_loudly_without_gpu(pt):
     if pt.device_count() > 0:
         pytest.skip("a GPU is visible")
