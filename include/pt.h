@@ -119,10 +119,17 @@ int pt_write_png_rgba8(const char* path, const uint8_t* rgba, int width, int hei
  * copyObjMatsToDevice, one copyTrianglesToDevice<<<1,1>>> per triangle). */
 int pt_scene_create(int device, const pt_object* objs, int64_t n_objects,
                     const pt_material* mats, int64_t n_materials, pt_scene** out);
-/* Replaces lbvh::buildBVH (bvh.h:132-145).  flags: PT_BVH_ORIGIN_BOUNDS (default behaviour
- * of the reference: Morton bounds contain the origin).  Internal boxes are tight. */
+/* Replaces lbvh::buildBVH (bvh.h:132-145), entirely on the device: scene box, Morton codes
+ * (morton_code.h:19-45), a stable radix sort by code (the reference's host std::stable_sort,
+ * morton_code.h:64-75), leaf records, Karras hierarchy (bvh.h:17-115), bottom-up refit with
+ * tight internal boxes (growBBox, bvh.h:117-130).  flags: PT_BVH_ORIGIN_BOUNDS (default
+ * behaviour of the reference: the Morton bounds contain the origin, main.cu:122);
+ * PT_BVH_HOST_KEYS computes and sorts the keys on the host instead (identical result; A/B). */
 #define PT_BVH_ORIGIN_BOUNDS 1
+#define PT_BVH_HOST_KEYS 2
 int pt_scene_build_bvh(pt_scene* scene, int flags);
+/* Device time of the last pt_scene_build_bvh (HIP events around the build's stream work). */
+int pt_scene_build_time(pt_scene* scene, double* ms);
 int pt_scene_bvh_info(pt_scene* scene, int* depth, int64_t* n_nodes, int64_t* device_bytes);
 /* Download the LBVH in the reference's node layout (2n-1 nodes). */
 int pt_scene_download_bvh(pt_scene* scene, pt_bvh_node* nodes);

@@ -31,6 +31,11 @@
 
 using pt::fail;
 
+namespace pt {   // pt_sort.hip
+hipError_t radixSortPairs(void* temp, size_t* temp_bytes, const uint32_t* codes_in, uint32_t* codes_out,
+                          const uint32_t* ids_in, uint32_t* ids_out, size_t n, int bits, hipStream_t stream);
+}
+
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
         hipError_t _e = (expr);                                                              \
@@ -1390,6 +1395,133 @@ __global__ void refitKernel(float4* nodes, const int* __restrict__ iparent, cons
     (void)childRef;
 }
 
+// --- Morton keys and leaf records on the device (morton_code.h:19-75, cuda_object.h:21-42) ----
+// Each expression restates the host computation (pt_host.cpp mortonKeys / the leaf loop of
+// pt_scene_build_bvh) in the same operation order, so keys, boxes and normals are bit-identical.
+
+// Object box (cuda_object.h:21-42): sphere c -/+ |r|; triangle utils::unionPoints by comparisons.
+__device__ __forceinline__ void objBoxDev(const pt_object& o, float mn[3], float mx[3]) {
+    if (o.type == PT_SPHERE) {
+        const float r = fabsf(o.v[3]);
+        for (int a = 0; a < 3; a++) { mn[a] = o.v[a] - r; mx[a] = o.v[a] + r; }
+        return;
+    }
+    for (int a = 0; a < 3; a++) {
+        mn[a] = o.v[a];
+        mx[a] = o.v[a];
+    }
+    for (int k = 1; k < 3; k++)
+        for (int a = 0; a < 3; a++) {
+            const float p = o.v[3 * k + a];
+            if (mn[a] > p) mn[a] = p;
+            if (mx[a] < p) mx[a] = p;
+        }
+}
+
+// Scene box for the Morton quantisation (main.cu:122 + aabb::unionBoxInPlace, aabb.h:36-44):
+// min/max are exact and order-independent, so one workgroup reduces all boxes.  The reference
+// seeds the box with aabb() = the zero box (includeOrigin), or the first object's box.
+__global__ __launch_bounds__(1024) void sceneBoxKernel(const pt_object* __restrict__ objs, int64_t n,
+                                                       int includeOrigin, float* box6) {
+    __shared__ float red[6][1024];
+    float b[6];
+    if (includeOrigin) {
+        for (int a = 0; a < 6; a++) b[a] = 0.0f;
+    } else {
+        objBoxDev(objs[0], b, b + 3);
+    }
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        float mn[3], mx[3];
+        objBoxDev(objs[i], mn, mx);
+        for (int a = 0; a < 3; a++) {
+            b[a] = fminf(b[a], mn[a]);
+            b[3 + a] = fmaxf(b[3 + a], mx[a]);
+        }
+    }
+    for (int a = 0; a < 6; a++) red[a][threadIdx.x] = b[a];
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int a = 0; a < 3; a++) {
+                red[a][threadIdx.x] = fminf(red[a][threadIdx.x], red[a][threadIdx.x + w]);
+                red[3 + a][threadIdx.x] = fmaxf(red[3 + a][threadIdx.x], red[3 + a][threadIdx.x + w]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) box6[threadIdx.x] = red[threadIdx.x][0];
+}
+
+__device__ __forceinline__ uint32_t expandBitsDev(uint32_t v) {   // morton_code.h:19-27
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+// mortonCode3D (morton_code.h:29-45): centre normalised into the scene box (an axis whose
+// range is <= 1e-7 maps to 0), x1024, clamped to [0, 1023], truncated, interleaved.
+__global__ __launch_bounds__(256) void mortonKernel(const pt_object* __restrict__ objs, int64_t n,
+                                                    const float* __restrict__ box6, uint32_t* codes, uint32_t* ids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float mn[3], mx[3];
+    objBoxDev(objs[i], mn, mx);
+    uint32_t q[3];
+    for (int a = 0; a < 3; a++) {
+        const float smn = box6[a], range = box6[3 + a] - box6[a];
+        const float c = (mn[a] + mx[a]) * 0.5f;
+        float x = 0.0f;
+        if ((double)range > 1e-7) x = (c - smn) / range;
+        q[a] = (uint32_t)fminf(fmaxf(x * 1024.0f, 0.0f), 1023.0f);
+    }
+    codes[i] = (expandBitsDev(q[0]) << 2) + (expandBitsDev(q[1]) << 1) + expandBitsDev(q[2]);
+    ids[i] = (uint32_t)i;
+}
+
+// Leaf k of the sorted order: the 64-bit key (code << 32 | objID, the MORTON64 union of
+// morton_code.h), the primitive record, the triangle normal (triangle.h:17-19:
+// normalize(cross(v1 - v0, v2 - v0))), the exact leaf box and the sphere flag.
+__global__ __launch_bounds__(256) void leafGatherKernel(const pt_object* __restrict__ objs,
+                                                        const uint32_t* __restrict__ codes,
+                                                        const uint32_t* __restrict__ ids, int64_t n,
+                                                        unsigned long long* keys, float4* prims, float4* normals,
+                                                        float* boxes, uint32_t* sphereFlag) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t id = ids[k];
+    const pt_object o = objs[id];
+    keys[k] = ((unsigned long long)codes[k] << 32) | id;
+    float mn[3], mx[3];
+    objBoxDev(o, mn, mx);
+    for (int a = 0; a < 3; a++) { boxes[6 * k + a] = mn[a]; boxes[6 * k + 3 + a] = mx[a]; }
+    if (o.type == PT_SPHERE) {
+        prims[3 * k] = make_float4(o.v[0], o.v[1], o.v[2], __uint_as_float((uint32_t)o.mat));
+        prims[3 * k + 1] = make_float4(o.v[3], 0.0f, 0.0f, __uint_as_float(id));
+        prims[3 * k + 2] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(1u));
+        normals[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        sphereFlag[k] = 1u;
+    } else {
+        const float3 v0 = f3(o.v[0], o.v[1], o.v[2]), v1 = f3(o.v[3], o.v[4], o.v[5]), v2 = f3(o.v[6], o.v[7], o.v[8]);
+        const float3 nn = normalize3(cross3(sub(v1, v0), sub(v2, v0)));
+        prims[3 * k] = make_float4(v0.x, v0.y, v0.z, __uint_as_float((uint32_t)o.mat));
+        prims[3 * k + 1] = make_float4(v1.x, v1.y, v1.z, __uint_as_float(id));
+        prims[3 * k + 2] = make_float4(v2.x, v2.y, v2.z, 0.0f);
+        normals[k] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+        sphereFlag[k] = 0u;
+    }
+}
+
+// Depth of the internal hierarchy (root = 1) = the most internal ancestors of any leaf.
+__global__ __launch_bounds__(256) void depthKernel(const int* __restrict__ iparent, const int* __restrict__ lparent,
+                                                   int n, int* depth) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int d = 0;
+    for (int p = lparent[k]; p >= 0 && d <= n; p = iparent[p]) d++;
+    atomicMax(depth, d);
+}
+
 // ------------------------------------------------------------------------ host helpers
 // GF(2) 160x160 jump matrices for XORWOW's xorshift part (product-side implementation).
 struct Mat160 { uint32_t c[160][5]; };
@@ -1436,6 +1568,7 @@ struct DevBuf {
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     template <class T> T* as() const { return static_cast<T*>(p); }
+    void reset() { if (p) (void)hipFree(p); p = nullptr; }
 };
 
 int devAlloc(DevBuf& b, size_t bytes) {
@@ -1470,17 +1603,17 @@ int stackFor(int depth) {
 struct pt_scene {
     int device = 0;
     int64_t nobj = 0, nmat = 0;
-    std::vector<pt_object> objs;            // host copy (BVH build input)
+    std::vector<pt_object> objs;            // host copy (PT_BVH_HOST_KEYS path)
+    DevBuf dobjs;                           // the objects on the device (BVH build input)
     DevBuf mats, nodes, prims, normals, counters;
-    std::vector<uint64_t> keys;             // sorted Morton keys of the current BVH
-    std::vector<int32_t> iparent, lparent;  // host copies for download
-    std::vector<float> leafBoxes;           // 6 floats per leaf slot
-    DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelW4)
+    DevBuf keys, iparent, lparent, leafBoxes;   // sorted 64-bit Morton keys, parent links, leaf boxes
+    DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelW4), built on first use
     int wideDepth = 0;
     int64_t wideNodes = 0;
     int depth = 0;
     bool built = false;
     size_t deviceBytes = 0;
+    double buildMs = 0.0;                   // last pt_scene_build_bvh, device time (HIP events)
 };
 
 struct pt_film {
@@ -1721,6 +1854,8 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
     if ((rc = devAlloc(s->mats, m.size() * sizeof(float4)))) return rc;
     HIP_TRY(hipMemcpy(s->mats.p, m.data(), m.size() * sizeof(float4), hipMemcpyHostToDevice));
     if ((rc = devAlloc(s->counters, 16 * sizeof(unsigned long long)))) return rc;
+    if ((rc = devAlloc(s->dobjs, (size_t)std::max<int64_t>(1, n) * sizeof(pt_object)))) return rc;
+    if (n > 0) HIP_TRY(hipMemcpy(s->dobjs.p, objs, (size_t)n * sizeof(pt_object), hipMemcpyHostToDevice));
     *out = s.release();
     return PT_OK;
 }
@@ -1731,103 +1866,103 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     if (rc) return rc;
     const int64_t n = s->nobj;
     s->built = false;
-    s->keys.assign((size_t)n, 0);
-    if (n > 0) pt::mortonKeys(s->objs.data(), n, (flags & PT_BVH_ORIGIN_BOUNDS) != 0, s->keys.data());
-    // primitives in leaf order: (v0|c, mat) (e1|r, obj) (e2, isSphere); leaf boxes (cuda_object.h:21-42)
-    std::vector<float4> prims((size_t)std::max<int64_t>(1, 3 * n)), normals((size_t)std::max<int64_t>(1, n));
-    std::vector<float> boxes((size_t)std::max<int64_t>(1, 6 * n));
-    std::vector<uint32_t> sphereFlag((size_t)std::max<int64_t>(1, n));
-    auto bits = [](uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; };
-    for (int64_t k = 0; k < n; k++) {
-        const uint32_t id = (uint32_t)(s->keys[k] & 0xffffffffu);
-        const pt_object& o = s->objs[id];
-        float* bx = &boxes[6 * k];
-        if (o.type == PT_SPHERE) {
-            prims[3 * k] = make_float4(o.v[0], o.v[1], o.v[2], bits((uint32_t)o.mat));
-            prims[3 * k + 1] = make_float4(o.v[3], 0.0f, 0.0f, bits(id));
-            prims[3 * k + 2] = make_float4(0.0f, 0.0f, 0.0f, bits(1u));
-            normals[k] = make_float4(0, 0, 0, 0);
-            const float r = std::fabs(o.v[3]);
-            for (int a = 0; a < 3; a++) { bx[a] = o.v[a] - r; bx[3 + a] = o.v[a] + r; }
-            sphereFlag[k] = 1;
+    s->wide.reset();
+    s->wideNodes = 0;
+    s->wideDepth = 0;
+    // Everything on the device, on one stream: scene box -> Morton codes -> radix sort ->
+    // leaf records -> Karras hierarchy -> refit -> depth.  (PT_BVH_HOST_KEYS: the keys come from
+    // the host restatement of computeMortonOnHost instead; the result is identical.)
+    const size_t n1 = (size_t)std::max<int64_t>(1, n), ni = (size_t)std::max<int64_t>(1, n - 1);
+    if ((rc = devAlloc(s->prims, n1 * 3 * sizeof(float4))) || (rc = devAlloc(s->normals, n1 * sizeof(float4))) ||
+        (rc = devAlloc(s->nodes, ni * 4 * sizeof(float4))) || (rc = devAlloc(s->keys, n1 * 8)) ||
+        (rc = devAlloc(s->leafBoxes, n1 * 24)) || (rc = devAlloc(s->iparent, ni * 4)) ||
+        (rc = devAlloc(s->lparent, n1 * 4)))
+        return rc;
+    DevBuf codes, ids, codes2, ids2, box6, sph, arr, dep, temp;
+    if ((rc = devAlloc(codes, n1 * 4)) || (rc = devAlloc(ids, n1 * 4)) || (rc = devAlloc(codes2, n1 * 4)) ||
+        (rc = devAlloc(ids2, n1 * 4)) || (rc = devAlloc(box6, 64)) || (rc = devAlloc(sph, n1 * 4)) ||
+        (rc = devAlloc(arr, ni * 4)) || (rc = devAlloc(dep, 16)))
+        return rc;
+    hipStream_t st = 0;
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+    const unsigned tb = 256, nb = (unsigned)((n1 + tb - 1) / tb), nbi = (unsigned)((ni + tb - 1) / tb);
+    if (n > 0) {
+        if (flags & PT_BVH_HOST_KEYS) {
+            std::vector<uint64_t> hk((size_t)n);
+            pt::mortonKeys(s->objs.data(), n, (flags & PT_BVH_ORIGIN_BOUNDS) != 0, hk.data());
+            std::vector<uint32_t> hc((size_t)n), hi((size_t)n);
+            for (int64_t k = 0; k < n; k++) { hc[k] = (uint32_t)(hk[k] >> 32); hi[k] = (uint32_t)hk[k]; }
+            HIP_TRY(hipMemcpyAsync(codes2.p, hc.data(), n * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(ids2.p, hi.data(), n * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));
         } else {
-            const pt::vec3 v0(o.v[0], o.v[1], o.v[2]), v1(o.v[3], o.v[4], o.v[5]), v2(o.v[6], o.v[7], o.v[8]);
-            const pt::vec3 nn = pt::normalize(pt::cross(v1 - v0, v2 - v0));   // triangle.h:17-19
-            prims[3 * k] = make_float4(v0.x(), v0.y(), v0.z(), bits((uint32_t)o.mat));
-            prims[3 * k + 1] = make_float4(v1.x(), v1.y(), v1.z(), bits(id));
-            prims[3 * k + 2] = make_float4(v2.x(), v2.y(), v2.z(), bits(0u));
-            normals[k] = make_float4(nn.x(), nn.y(), nn.z(), 0.0f);
-            for (int a = 0; a < 3; a++) {
-                float mn = o.v[a], mx = o.v[a];
-                for (int q = 1; q < 3; q++) {
-                    if (mn > o.v[3 * q + a]) mn = o.v[3 * q + a];
-                    if (mx < o.v[3 * q + a]) mx = o.v[3 * q + a];
-                }
-                bx[a] = mn;
-                bx[3 + a] = mx;
-            }
-            sphereFlag[k] = 0;
+            sceneBoxKernel<<<1, 1024, 0, st>>>(s->dobjs.as<pt_object>(), n, (flags & PT_BVH_ORIGIN_BOUNDS) ? 1 : 0,
+                                               box6.as<float>());
+            mortonKernel<<<nb, tb, 0, st>>>(s->dobjs.as<pt_object>(), n, box6.as<float>(), codes.as<uint32_t>(),
+                                            ids.as<uint32_t>());
+            HIP_TRY(hipGetLastError());
+            size_t tbytes = 0;
+            HIP_TRY(pt::radixSortPairs(nullptr, &tbytes, codes.as<uint32_t>(), codes2.as<uint32_t>(),
+                                       ids.as<uint32_t>(), ids2.as<uint32_t>(), (size_t)n, 30, st));
+            if ((rc = devAlloc(temp, tbytes))) return rc;
+            HIP_TRY(pt::radixSortPairs(temp.p, &tbytes, codes.as<uint32_t>(), codes2.as<uint32_t>(),
+                                       ids.as<uint32_t>(), ids2.as<uint32_t>(), (size_t)n, 30, st));
         }
+        leafGatherKernel<<<nb, tb, 0, st>>>(s->dobjs.as<pt_object>(), codes2.as<uint32_t>(), ids2.as<uint32_t>(), n,
+                                            s->keys.as<unsigned long long>(), s->prims.as<float4>(),
+                                            s->normals.as<float4>(), s->leafBoxes.as<float>(), sph.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
     }
-    s->leafBoxes = boxes;
-    const int64_t ni = std::max<int64_t>(0, n - 1);
-    if ((rc = devAlloc(s->prims, prims.size() * sizeof(float4)))) return rc;
-    if ((rc = devAlloc(s->normals, normals.size() * sizeof(float4)))) return rc;
-    if ((rc = devAlloc(s->nodes, (size_t)std::max<int64_t>(1, ni) * 4 * sizeof(float4)))) return rc;
-    HIP_TRY(hipMemcpy(s->prims.p, prims.data(), prims.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(s->normals.p, normals.data(), normals.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(s->nodes.p, 0, (size_t)std::max<int64_t>(1, ni) * 4 * sizeof(float4)));
-    s->iparent.assign((size_t)std::max<int64_t>(1, ni), -1);
-    s->lparent.assign((size_t)std::max<int64_t>(1, n), -1);
-    s->depth = 0;
+    HIP_TRY(hipMemsetAsync(s->nodes.p, 0, ni * 4 * sizeof(float4), st));
+    HIP_TRY(hipMemsetAsync(s->iparent.p, 0xff, ni * 4, st));
+    HIP_TRY(hipMemsetAsync(s->lparent.p, 0xff, n1 * 4, st));
+    HIP_TRY(hipMemsetAsync(arr.p, 0, ni * 4, st));
+    HIP_TRY(hipMemsetAsync(dep.p, 0, 16, st));
     if (n > 1) {
-        DevBuf dkeys, dip, dlp, dbox, darr, dsph;
-        if ((rc = devAlloc(dkeys, n * 8)) || (rc = devAlloc(dip, ni * 4)) || (rc = devAlloc(dlp, n * 4)) ||
-            (rc = devAlloc(dbox, n * 24)) || (rc = devAlloc(darr, ni * 4)) || (rc = devAlloc(dsph, n * 4)))
-            return rc;
-        HIP_TRY(hipMemcpy(dkeys.p, s->keys.data(), n * 8, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(dbox.p, boxes.data(), n * 24, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(dsph.p, sphereFlag.data(), n * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemset(dip.p, 0xff, ni * 4));
-        HIP_TRY(hipMemset(dlp.p, 0xff, n * 4));
-        HIP_TRY(hipMemset(darr.p, 0, ni * 4));
-        const int tb = 256;
-        karrasKernel<<<(unsigned)((ni + tb - 1) / tb), tb>>>(dkeys.as<unsigned long long>(), (int)n,
-                                                                s->nodes.as<float4>(), dip.as<int>(), dlp.as<int>(),
-                                                                dsph.as<uint32_t>());
+        karrasKernel<<<nbi, tb, 0, st>>>(s->keys.as<unsigned long long>(), (int)n, s->nodes.as<float4>(),
+                                         s->iparent.as<int>(), s->lparent.as<int>(), sph.as<uint32_t>());
         HIP_TRY(hipGetLastError());
-        refitKernel<<<(unsigned)((n + tb - 1) / tb), tb>>>(s->nodes.as<float4>(), dip.as<int>(), dlp.as<int>(),
-                                                             dbox.as<float>(), darr.as<unsigned int>(), (int)n);
+        refitKernel<<<nb, tb, 0, st>>>(s->nodes.as<float4>(), s->iparent.as<int>(), s->lparent.as<int>(),
+                                       s->leafBoxes.as<float>(), arr.as<unsigned int>(), (int)n);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemcpy(s->iparent.data(), dip.p, ni * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(s->lparent.data(), dlp.p, n * 4, hipMemcpyDeviceToHost));
-        // depth of the internal hierarchy (root = 1): picks the LDS stack size
-        std::vector<int> d((size_t)ni, 0);
-        std::vector<float4> tmp((size_t)ni * 4);
-        HIP_TRY(hipMemcpy(tmp.data(), s->nodes.p, ni * 4 * sizeof(float4), hipMemcpyDeviceToHost));
-        d[0] = 1;
-        int maxd = 1;
-        std::vector<int> st{0};
-        while (!st.empty()) {
-            int i = st.back();
-            st.pop_back();
-            for (float f : {tmp[4 * i + 3].x, tmp[4 * i + 3].y}) {
-                uint32_t r;
-                std::memcpy(&r, &f, 4);
-                if (!(r & kLeafBit)) {
-                    d[r] = d[i] + 1;
-                    maxd = std::max(maxd, d[r]);
-                    st.push_back((int)r);
-                }
-            }
-        }
-        s->depth = maxd;
-        if ((rc = buildWide4(s, tmp))) return rc;
+        depthKernel<<<nb, tb, 0, st>>>(s->iparent.as<int>(), s->lparent.as<int>(), (int)n, dep.as<int>());
+        HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    s->buildMs = ms;
+    int depth = 0;
+    HIP_TRY(hipMemcpy(&depth, dep.p, 4, hipMemcpyDeviceToHost));
+    s->depth = n > 1 ? depth : 0;
     if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
-    s->deviceBytes = (size_t)ni * 64 + (size_t)n * 64 + (size_t)s->nmat * 32;
+    s->deviceBytes = (size_t)(n > 1 ? n - 1 : 0) * 64 + (size_t)n * 64 + (size_t)s->nmat * 32;
     s->built = true;
+    return PT_OK;
+}
+
+// The 4-wide collapse is only needed by PT_KERNEL_WIDE: built from the device LBVH on first use.
+static int ensureWide(pt_scene* s) {
+    if (s->wide.p || s->nobj <= 1) return PT_OK;
+    const size_t ni = (size_t)(s->nobj - 1);
+    std::vector<float4> tmp(ni * 4);
+    HIP_TRY(hipMemcpy(tmp.data(), s->nodes.p, ni * 4 * sizeof(float4), hipMemcpyDeviceToHost));
+    int rc = buildWide4(s, tmp);
+    if (rc) return rc;
+    if (stackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");
+    return PT_OK;
+}
+
+int pt_scene_build_time(pt_scene* s, double* ms) {
+    if (!s || !ms) return fail(PT_ERR_INVALID, "pt_scene_build_time: null argument");
+    if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
+    *ms = s->buildMs;
     return PT_OK;
 }
 
@@ -1848,16 +1983,23 @@ int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
     const int64_t n = s->nobj;
     if (n <= 0) return PT_OK;
     const int64_t L = n - 1;
-    std::vector<float4> nodes((size_t)std::max<int64_t>(1, L) * 4), prims((size_t)n * 3);
+    std::vector<float4> nodes((size_t)std::max<int64_t>(1, L) * 4);
+    std::vector<uint64_t> keys((size_t)n);
+    std::vector<int32_t> iparent((size_t)std::max<int64_t>(1, L)), lparent((size_t)n);
+    std::vector<float> leafBoxes((size_t)n * 6);
     if (L > 0) HIP_TRY(hipMemcpy(nodes.data(), s->nodes.p, L * 4 * sizeof(float4), hipMemcpyDeviceToHost));
+    if (L > 0) HIP_TRY(hipMemcpy(iparent.data(), s->iparent.p, L * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(keys.data(), s->keys.p, n * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lparent.data(), s->lparent.p, n * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(leafBoxes.data(), s->leafBoxes.p, n * 24, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < 2 * n - 1; i++) {
         out[i].left = out[i].right = out[i].parent = out[i].objid = -1;
         for (int a = 0; a < 3; a++) out[i].bmin[a] = out[i].bmax[a] = 0.0f;
     }
     auto refIndex = [&](uint32_t r) -> int64_t { return (r & kLeafBit) ? L + (int64_t)(r & kPrimMask) : (int64_t)r; };
     for (int64_t k = 0; k < n; k++) {
-        out[L + k].objid = (int32_t)(s->keys[k] & 0xffffffffu);
-        out[L + k].parent = L > 0 ? s->lparent[k] : -1;
+        out[L + k].objid = (int32_t)(keys[k] & 0xffffffffu);
+        out[L + k].parent = L > 0 ? lparent[k] : -1;
     }
     for (int64_t i = 0; i < L; i++) {
         const float* f = reinterpret_cast<const float*>(&nodes[4 * i]);
@@ -1866,7 +2008,7 @@ int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
         std::memcpy(&rr, f + 13, 4);
         out[i].left = (int32_t)refIndex(lr);
         out[i].right = (int32_t)refIndex(rr);
-        out[i].parent = i == 0 ? -1 : s->iparent[i];
+        out[i].parent = i == 0 ? -1 : iparent[i];
         for (int c = 0; c < 2; c++) {   // child boxes live in this record; copy them to the child
             pt_bvh_node& ch = out[c == 0 ? out[i].left : out[i].right];
             for (int a = 0; a < 3; a++) { ch.bmin[a] = f[6 * c + a]; ch.bmax[a] = f[6 * c + 3 + a]; }
@@ -1879,7 +2021,7 @@ int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
         }
     }
     if (L == 0) {   // single object: the root is the leaf (bvh.h:76-81 with numObjects = 1)
-        for (int a = 0; a < 3; a++) { out[0].bmin[a] = s->leafBoxes[a]; out[0].bmax[a] = s->leafBoxes[3 + a]; }
+        for (int a = 0; a < 3; a++) { out[0].bmin[a] = leafBoxes[a]; out[0].bmax[a] = leafBoxes[3 + a]; }
     }
     return PT_OK;
 }
@@ -2074,13 +2216,18 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     }
     if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
         return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
-    if (kernel == PT_KERNEL_WIDE && s->nobj > 1 && !s->wide.p) return fail(PT_ERR_STATE, "wide BVH missing");
+
     const int rng = opts ? opts->rng : PT_RNG_COMPAT;
     if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
     if (rng == PT_RNG_SAMPLE && kernel == PT_KERNEL_WIDE) {
         if (opts && opts->kernel != PT_KERNEL_DEFAULT)
             return fail(PT_ERR_INVALID, "pt_render_ex: sample mode runs on the wavefront or simple kernel");
         kernel = PT_KERNEL_WAVEFRONT;
+    }
+    if (kernel == PT_KERNEL_WIDE) {
+        if ((rc = ensureWide(s))) return rc;
+        P.S = devScene(s);   // now with the wide nodes
+        if (s->nobj > 1 && !P.S.wnodes) return fail(PT_ERR_STATE, "wide BVH missing");
     }
     P.kernel = kernel;
     P.nblocks = 0;

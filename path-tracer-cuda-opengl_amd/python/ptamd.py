@@ -21,7 +21,7 @@ MODELS_DIR = os.path.join(REPO, "models")
 PT_OK = 0
 PT_SPHERE, PT_TRIANGLE = 1, 3
 PT_LAMBERTIAN, PT_METAL, PT_DIELECTRIC = 1, 2, 4
-PT_BVH_ORIGIN_BOUNDS = 1
+PT_BVH_ORIGIN_BOUNDS, PT_BVH_HOST_KEYS = 1, 2
 
 # numpy mirrors of the C structs (all 4-byte fields, no padding)
 OBJECT_DTYPE = np.dtype([("type", "<i4"), ("mat", "<i4"), ("v", "<f4", (9,))])
@@ -76,7 +76,7 @@ EXPORTS = [
     "pt_quantize_rgba8", "pt_scene_create", "pt_scene_build_bvh", "pt_scene_bvh_info", "pt_scene_download_bvh",
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
-    "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8",
+    "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -100,6 +100,7 @@ _sig = {
     "pt_quantize_rgba8": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "pt_scene_create": (C.c_int, [C.c_int, _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_void_p)]),
     "pt_scene_build_bvh": (C.c_int, [_P, C.c_int]),
+    "pt_scene_build_time": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "pt_scene_bvh_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "pt_scene_download_bvh": (C.c_int, [_P, _P]),
     "pt_trace_closest": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, _P, C.POINTER(Stats)]),
@@ -240,6 +241,13 @@ class Scene:
 
     def build_bvh(self, flags: int = PT_BVH_ORIGIN_BOUNDS) -> None:
         _check(lib.pt_scene_build_bvh(self.h, flags), "pt_scene_build_bvh")
+
+    @property
+    def build_ms(self) -> float:
+        """Device time of the last LBVH build (HIP events)."""
+        ms = C.c_double()
+        _check(lib.pt_scene_build_time(self.h, C.byref(ms)), "pt_scene_build_time")
+        return ms.value
 
     def bvh_info(self) -> dict:
         d, n, b = C.c_int(), C.c_int64(), C.c_int64()
