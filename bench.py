@@ -104,6 +104,10 @@ def main() -> None:
                          "reference's per-pixel cuRAND-XORWOW streams (a pixel's 1024 samples are sequential)")
     ap.add_argument("--chunk", type=int, default=0, help="sample mode: summation block (0 = library default)")
     ap.add_argument("--no-compat", action="store_true", help="skip the compat-mode reference frame (N = 1)")
+    ap.add_argument("--output", default="rgba8", choices=["rgba8", "f32"],
+                    help="frame format rendered and gathered: rgba8 (default: quantised on the device like "
+                         "PngImage::saveColor, 4 B/pixel on the wire) or f32 (linear-sqrt RGB, 12 B/pixel)")
+    ap.add_argument("--png", default="", help="rank 0 writes the last (assembled) frame to this PNG")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,8 +127,11 @@ def main() -> None:
     scene = ptamd.Scene(preset.objects, preset.materials, device=local)
     film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
     max_rows = ptdist.max_rows(h, STRIPE, world)
-    local_buf = torch.zeros((max_rows * w * 3,), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world * max_rows * w * 3,), dtype=torch.float32, device=dev) if world > 1 else None
+    rgba8 = args.output == "rgba8"
+    chans, tdt = (4, torch.uint8) if rgba8 else (3, torch.float32)
+    out_format = ptamd.OUT_RGBA8 if rgba8 else ptamd.OUT_RGB32F
+    local_buf = torch.zeros((max_rows * w * chans,), dtype=tdt, device=dev)
+    gathered = torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
     sample = args.rng == "sample"
@@ -137,7 +144,7 @@ def main() -> None:
         _, st = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
                              stream=stream.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
                              shade_batch=args.shade_batch, rng=ptamd.RNG_SAMPLE if sample else ptamd.RNG_COMPAT,
-                             chunk=args.chunk)
+                             chunk=args.chunk, out_format=out_format)
         if world > 1:
             dist.all_gather_into_tensor(gathered, local_buf)
         return st
@@ -188,7 +195,7 @@ def main() -> None:
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
             _, cst = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
-                                  stream=stream.cuda_stream, rng=ptamd.RNG_COMPAT)
+                                  stream=stream.cuda_stream, rng=ptamd.RNG_COMPAT, out_format=out_format)
             torch.cuda.synchronize(dev)
             el1 = time.perf_counter() - t1
         compat = {"value": cst.rays / el1 / 1e6, "unit": "Mray/s", "ms_per_step": el1 * 1e3,
@@ -198,8 +205,16 @@ def main() -> None:
 
     if rank == 0:
         if world > 1:   # un-permute the stripes of the last frame (rank 0 holds the full image)
-            ptdist.assemble(gathered, h, w, STRIPE, world)
+            img = ptdist.assemble(gathered, h, w, STRIPE, world, chans)
             torch.cuda.synchronize(dev)
+        else:
+            img = local_buf[: h * w * chans]
+        if args.png:
+            a = img.reshape(-1).cpu().numpy()
+            if rgba8:
+                ptamd.write_png_rgba8(args.png, a, w, h)
+            else:
+                ptamd.write_png(args.png, a, w, h)
         achieved = (kbytes / 1e9) / (kms / 1e3) if kms > 0 else 0.0
         rng_desc = (("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
                      f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
@@ -220,6 +235,8 @@ def main() -> None:
             "data": "synthetic: scene assembled from the reference's bundled OBJ models (models/), fixed seed",
             "config": {"workload": workload, "width": w, "height": h, "spp": spp, "max_depth": depth,
                        "stripe_rows": STRIPE, "parallelism": f"rows{world}",
+                       "output": ("rgba8: quantised on the device like PngImage::saveColor, gathered at 4 B/pixel"
+                                  if rgba8 else "f32 RGB, gathered at 12 B/pixel"),
                        "rays_per_frame": total_rays / args.steps,
                        "rng": ("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
                                f"block {args.chunk or max(16, -(-spp // 64))}") if sample else

@@ -17,6 +17,9 @@ static void usage() {
     std::fprintf(stderr,
                  "usage: pt_render_png [--scene NAME] [--models DIR] [--width W] [--height H] [--spp N]\n"
                  "                     [--depth D] [--seed S] [--gpus N] [--stripe ROWS] [--out FILE]\n"
+                 "                     [--rng compat|sample] [--frames K]\n"
+                 "--frames K: progressive rendering, K frames of --spp samples accumulated per pixel (the\n"
+                 "            headless counterpart of the reference's interactive loop); PNG of the last one\n"
                  "scenes: triangle_world (default, as the reference), random_world, test_world, rtiow,\n"
                  "        cornell, bunny_cornell, bunny_field\n");
 }
@@ -32,7 +35,7 @@ static void usage() {
 
 int main(int argc, char** argv) {
     std::string scene = "triangle_world", models = "models", out = "debug.png";
-    int width = 0, height = 0, spp = -1, depth = -1, gpus = 1, stripe = 8;
+    int width = 0, height = 0, spp = -1, depth = -1, gpus = 1, stripe = 8, frames = 1, rng = PT_RNG_COMPAT;
     unsigned long long seed = 1;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
@@ -50,6 +53,13 @@ int main(int argc, char** argv) {
         else if (a == "--gpus") gpus = std::atoi(next());
         else if (a == "--stripe") stripe = std::atoi(next());
         else if (a == "--out") out = next();
+        else if (a == "--frames") frames = std::atoi(next());
+        else if (a == "--rng") {
+            std::string r = next();
+            if (r == "compat") rng = PT_RNG_COMPAT;
+            else if (r == "sample") rng = PT_RNG_SAMPLE;
+            else { usage(); return 2; }
+        }
         else { usage(); return 2; }
     }
     pt_scene_desc d;
@@ -63,8 +73,12 @@ int main(int argc, char** argv) {
     std::printf("scene %s: %lld objects, %dx%d @%dspp depth %d on %d GPU(s)\n", d.name, (long long)d.n_objects,
                 d.width, d.height, d.spp, d.max_depth, gpus);
 
-    std::vector<float> frame((size_t)d.width * d.height * 3);
+    if (frames < 1) frames = 1;
+    // The frame is quantised on the device (PT_OUT_RGBA8: PngImage::saveColor per pixel), so each
+    // GPU hands back 4 bytes per pixel of its row stripes.
+    std::vector<uint8_t> frame((size_t)d.width * d.height * 4);
     std::vector<pt_stats> stats(gpus);
+    std::vector<double> kms(gpus, 0.0);
     std::vector<std::thread> th;
     auto t0 = std::chrono::steady_clock::now();
     for (int g = 0; g < gpus; g++) {
@@ -79,11 +93,23 @@ int main(int argc, char** argv) {
             CHECK(pt_film_info(f, &nrows, &npix));
             std::vector<int32_t> rows(nrows);
             CHECK(pt_film_rows(f, rows.data()));
-            std::vector<float> part((size_t)npix * 3);
-            CHECK(pt_render(s, f, &d.camera, d.spp, d.max_depth, part.data(), 0, nullptr, &stats[g]));
+            std::vector<uint8_t> part((size_t)npix * 4);
+            pt_render_opts o{};
+            o.rng = rng;
+            o.out_format = PT_OUT_RGBA8;
+            o.flags = frames > 1 ? PT_RENDER_ACCUMULATE : 0;
+            pt_stats st{};
+            for (int k = 0; k < frames; k++) {
+                CHECK(pt_render_ex(s, f, &d.camera, d.spp, d.max_depth, reinterpret_cast<float*>(part.data()), 0,
+                                   nullptr, &o, &st));
+                kms[g] += st.kernel_ms;
+                stats[g].rays += st.rays;
+                if (frames > 1 && g == 0)
+                    std::printf("frame %d: %d spp accumulated, %.2f ms kernel on GPU 0\n", k + 1, (k + 1) * d.spp,
+                                st.kernel_ms);
+            }
             for (int r = 0; r < nrows; r++)
-                std::memcpy(&frame[(size_t)rows[r] * d.width * 3], &part[(size_t)r * d.width * 3],
-                            sizeof(float) * 3 * d.width);
+                std::memcpy(&frame[(size_t)rows[r] * d.width * 4], &part[(size_t)r * d.width * 4], 4 * (size_t)d.width);
             pt_film_destroy(f);
             pt_scene_destroy(s);
         });
@@ -91,14 +117,14 @@ int main(int argc, char** argv) {
     for (auto& t : th) t.join();
     double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     unsigned long long rays = 0;
-    double kms = 0;
-    for (auto& s : stats) {
-        rays += s.rays;
-        kms = s.kernel_ms > kms ? s.kernel_ms : kms;
+    double kmax = 0;
+    for (int g = 0; g < gpus; g++) {
+        rays += stats[g].rays;
+        kmax = kms[g] > kmax ? kms[g] : kmax;
     }
-    std::printf("Time Cost: %.3f s kernel (max over GPUs), %.3f s wall incl. setup; %.1f Mray/s\n", kms / 1e3, wall,
-                rays / (kms * 1e3));
-    CHECK(pt_write_png(out.c_str(), frame.data(), d.width, d.height));
+    std::printf("Time Cost: %.3f s kernel (max over GPUs), %.3f s wall incl. setup; %.1f Mray/s\n", kmax / 1e3, wall,
+                rays / (kmax * 1e3));
+    CHECK(pt_write_png_rgba8(out.c_str(), frame.data(), d.width, d.height));
     pt_scene_desc_free(&d);
     return 0;
 }

@@ -2,7 +2,8 @@
 
 Stripe s (rows [s*stripe, (s+1)*stripe)) belongs to rank s % world, which interleaves cheap
 (sky) and expensive (geometry) rows across GPUs.  Every rank renders its rows packed in
-order into a buffer padded to `max_rows(...)` rows, one all-gather (RCCL over xGMI on the GPU
+order into a buffer padded to `max_rows(...)` rows (fp32 RGB, or RGBA8 quantised on the device:
+4 instead of 12 bytes per pixel on the wire), one all-gather (RCCL over xGMI on the GPU
 box, gloo in the CPU tests) concatenates the buffers, and `assemble` un-permutes them.
 The RNG is keyed by the GLOBAL pixel index (curand_init(seed, pixel, 0), main.cu:268), so
 the assembled frame is bit-identical to a single-GPU render.
@@ -22,21 +23,22 @@ def max_rows(height: int, stripe: int, world: int) -> int:
     return ((stripes + world - 1) // world) * stripe
 
 
-def assemble(gathered, height: int, width: int, stripe: int, world: int):
-    """gathered: array/tensor of shape (world, max_rows, width, 3) -> (height, width, 3)."""
+def assemble(gathered, height: int, width: int, stripe: int, world: int, channels: int = 3):
+    """gathered: array/tensor of shape (world, max_rows, width, channels) -> (height, width, channels).
+    channels = 3 for fp32 RGB frames, 4 for device-quantised RGBA8 frames (PT_OUT_RGBA8)."""
     mr = max_rows(height, stripe, world)
-    g = gathered.reshape(world, mr, width, 3)
+    g = gathered.reshape(world, mr, width, channels)
     try:  # torch tensor
         import torch
         if isinstance(g, torch.Tensor):
-            img = torch.empty((height, width, 3), dtype=g.dtype, device=g.device)
+            img = torch.empty((height, width, channels), dtype=g.dtype, device=g.device)
             for r in range(world):
                 rows = torch.as_tensor(stripe_rows(height, stripe, world, r), device=g.device, dtype=torch.long)
                 img[rows] = g[r, : len(rows)]
             return img
     except ImportError:
         pass
-    img = np.empty((height, width, 3), dtype=g.dtype)
+    img = np.empty((height, width, channels), dtype=g.dtype)
     for r in range(world):
         rows = stripe_rows(height, stripe, world, r)
         img[rows] = g[r, : len(rows)]

@@ -1,4 +1,7 @@
 """Scene / ray generators shared by the CPU and GPU test modules (seeded, deterministic)."""
+import struct
+import zlib
+
 import numpy as np
 
 OBJECT_DTYPE = np.dtype([("type", "<i4"), ("mat", "<i4"), ("v", "<f4", (9,))])
@@ -68,3 +71,22 @@ def rays_to_struct(rays: np.ndarray, ray_dtype) -> np.ndarray:
     out["o"] = rays[:, :3]
     out["d"] = rays[:, 3:]
     return out
+
+
+def read_png(path):
+    """Minimal reader for the 8-bit RGBA, filter-0 PNGs PngImage::write produces: (h, w, 4) uint8."""
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n, typ = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        assert zlib.crc32(typ + body) == struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])[0]
+        if typ == b"IHDR":
+            w, h = struct.unpack(">II", body[:8])
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 4 * w)
+    assert (raw[:, 0] == 0).all()
+    return raw[:, 1:].reshape(h, w, 4)

@@ -23,7 +23,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, w, h, stripe, spp, q):
+def _worker(rank, world, port, w, h, stripe, spp, q, rgba8=False):
     sys.path[:0] = [os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"), os.path.join(REPO, "oracle"), HERE]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -37,20 +37,25 @@ def _worker(rank, world, port, w, h, stripe, spp, q):
     rgb, st = oracle.render(p.objects, p.materials, nodes, ptamd.camera_to_array(p.camera), w, h, rows, spp, 50,
                             states, 1)
     mr = ptdist.max_rows(h, stripe, world)
-    buf = torch.zeros((mr * w * 3,), dtype=torch.float32)      # flat, as bench.py sends it
-    buf[: rgb.size] = torch.from_numpy(rgb.reshape(-1))
-    out = torch.empty((world * mr * w * 3,), dtype=torch.float32)
+    if rgba8:   # the device-quantised frame (PT_OUT_RGBA8), as bench.py sends it by default
+        px = oracle.quantize_png(rgb)
+        buf = torch.zeros((mr * w * 4,), dtype=torch.uint8)
+    else:
+        px = rgb
+        buf = torch.zeros((mr * w * 3,), dtype=torch.float32)      # flat
+    buf[: px.size] = torch.from_numpy(px.reshape(-1))
+    out = torch.empty((world * buf.numel(),), dtype=buf.dtype)
     dist.all_gather_into_tensor(out, buf)
     total = torch.tensor([float(st.rays)], dtype=torch.float64)
     dist.all_reduce(total)
     if rank == 0:
-        q.put((ptdist.assemble(out.numpy(), h, w, stripe, world), total.item()))
+        q.put((ptdist.assemble(out.numpy(), h, w, stripe, world, 4 if rgba8 else 3), total.item()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,stripe", [(2, 8), (3, 5)])
-def test_stripes_allgather_equals_single_rank(world, stripe):
+@pytest.mark.parametrize("world,stripe,rgba8", [(2, 8, False), (3, 5, False), (2, 4, True)])
+def test_stripes_allgather_equals_single_rank(world, stripe, rgba8):
     sys.path[:0] = [os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"), os.path.join(REPO, "oracle")]
     import oracle
     import ptamd
@@ -58,7 +63,7 @@ def test_stripes_allgather_equals_single_rank(world, stripe):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, stripe, spp, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, w, h, stripe, spp, q, rgba8)) for r in range(world)]
     for pr in procs:
         pr.start()
     try:
@@ -76,7 +81,10 @@ def test_stripes_allgather_equals_single_rank(world, stripe):
     rows = np.arange(h, dtype=np.int32)
     ref, st = oracle.render(p.objects, p.materials, nodes, ptamd.camera_to_array(p.camera), w, h, rows, spp, 50,
                             oracle.film_states(11, w, rows), 1)
-    np.testing.assert_array_equal(img.reshape(-1, 3).view(np.uint32), ref.view(np.uint32))
+    if rgba8:
+        np.testing.assert_array_equal(img.reshape(-1, 4), oracle.quantize_png(ref))
+    else:
+        np.testing.assert_array_equal(img.reshape(-1, 3).view(np.uint32), ref.view(np.uint32))
     assert rays == st.rays
 
 

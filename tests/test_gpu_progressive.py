@@ -153,3 +153,26 @@ def test_bad_format_rejected(pt, setup):
     film = pt.Film(W, H, seed=1)
     with pytest.raises(pt.PtError):
         pt.render(scene, film, p.camera, 1, DEPTH, out_format=7)
+
+
+@pytest.mark.parametrize("frames,rng", [(1, "compat"), (3, "sample")])
+def test_render_png_app(pt, orc, gpu, tmp_path, frames, rng):
+    """The C++ command-line app (main() -> renderToPng counterpart): device-quantised RGBA8
+    stripes written as a PNG equal the library's frame quantised on the host."""
+    import os
+    import subprocess
+    from helpers import read_png
+    app = os.path.join(os.path.dirname(pt.LIB_PATH), "pt_render_png")
+    out = str(tmp_path / "x.png")
+    w, h, spp = 64, 36, 2
+    r = subprocess.run([app, "--scene", "rtiow", "--models", pt.MODELS_DIR, "--width", str(w), "--height", str(h),
+                        "--spp", str(spp), "--depth", "50", "--seed", "7", "--frames", str(frames), "--rng", rng,
+                        "--out", out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    p = pt.Preset("rtiow", w, h)
+    scene = pt.Scene(p.objects, p.materials, device=gpu)
+    film = pt.Film(w, h, seed=7)
+    for _ in range(frames):
+        rgb, _ = pt.render(scene, film, p.camera, spp, 50, rng=pt.RNG_COMPAT if rng == "compat" else pt.RNG_SAMPLE,
+                           accumulate=frames > 1)
+    np.testing.assert_array_equal(read_png(out), pt.quantize_rgba8(rgb, w, h))
