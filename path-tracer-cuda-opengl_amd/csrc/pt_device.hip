@@ -53,7 +53,7 @@ constexpr int kJumpMats = 32;                    // XORWOW 2^(67+k) jump matrice
 
 // ------------------------------------------------------------------------ device structs
 struct DevScene {
-    const float4* nodes;     // 4 x float4 per internal node: lmin.xyz lmax.x | lmax.yz rmin.xy | rmin.z rmax.xyz | refs
+    const float4* nodes;     // 4 x float4 per internal node: child boxes as (min, max) pairs per axis, refs (nodeBoxIdx)
     const float4* prims;     // 3 x float4 per primitive (leaf order)
     const float4* normals;   // 1 x float4 per primitive (triangles)
     const float4* mats;      // 2 x float4 per material
@@ -156,6 +156,66 @@ __device__ __forceinline__ SlabHit slabLo(float mnx, float mny, float mnz, float
     float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
     float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
     return SlabHit{!(hi < lo), lo};
+}
+
+// Internal node record, 16 floats (4 x float4).  Each child box is stored as one (min, max)
+// pair per axis, so every pair sits in an aligned 64-bit register pair and the six slab
+// planes of a child cost three packed subtracts and three packed multiplies
+// (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations, two per instruction):
+//   [0..5]  left  {mnx, mxx, mny, mxy, mnz, mxz}     [6..11] right {mnx, mxx, mny, mxy, mnz, mxz}
+//   [12] left ref  [13] right ref  [14..15] unused
+__host__ __device__ constexpr int nodeBoxIdx(int child, int axis, int isMax) { return 6 * child + 2 * axis + isMax; }
+
+#ifndef PT_PACKED_SLAB
+#define PT_PACKED_SLAB 1
+#endif
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// slabLo on a box given as (min, max) pairs per axis (the node record layout).
+__device__ __forceinline__ SlabHit slabPair(v2f X, v2f Y, v2f Z, float3 o, float3 inv, float tmin, float tmax) {
+#if PT_PACKED_SLAB
+    const v2f tx = (X - o.x) * inv.x, ty = (Y - o.y) * inv.y, tz = (Z - o.z) * inv.z;
+#else
+    v2f tx, ty, tz;
+    tx.x = (X.x - o.x) * inv.x; tx.y = (X.y - o.x) * inv.x;
+    ty.x = (Y.x - o.y) * inv.y; ty.y = (Y.y - o.y) * inv.y;
+    tz.x = (Z.x - o.z) * inv.z; tz.y = (Z.y - o.z) * inv.z;
+#endif
+    float nx = inv.x < 0.0f ? tx.y : tx.x, fx = inv.x < 0.0f ? tx.x : tx.y;
+    float ny = inv.y < 0.0f ? ty.y : ty.x, fy = inv.y < 0.0f ? ty.x : ty.y;
+    float nz = inv.z < 0.0f ? tz.y : tz.x, fz = inv.z < 0.0f ? tz.x : tz.y;
+    float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
+    float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
+    return SlabHit{!(hi < lo), lo};
+}
+// Both child boxes of a node record at once (the 12 plane distances first, then the selects).
+struct SlabHit2 { SlabHit l, r; };
+__device__ __forceinline__ SlabHit2 slabBoth(float4 a, float4 b, float4 q, float3 o, float3 inv, float tmin,
+                                             float tmax) {
+    const v2f lx = (v2f{a.x, a.y} - o.x) * inv.x, ly = (v2f{a.z, a.w} - o.y) * inv.y,
+              lz = (v2f{b.x, b.y} - o.z) * inv.z;
+    const v2f rx = (v2f{b.z, b.w} - o.x) * inv.x, ry = (v2f{q.x, q.y} - o.y) * inv.y,
+              rz = (v2f{q.z, q.w} - o.z) * inv.z;
+    const bool sx = inv.x < 0.0f, sy = inv.y < 0.0f, sz = inv.z < 0.0f;
+    SlabHit2 h;
+    {
+        const float lo = fmaxf(fmaxf(fmaxf(tmin, sx ? lx.y : lx.x), sy ? ly.y : ly.x), sz ? lz.y : lz.x);
+        const float hi = fminf(fminf(fminf(tmax, sx ? lx.x : lx.y), sy ? ly.x : ly.y), sz ? lz.x : lz.y);
+        h.l = SlabHit{!(hi < lo), lo};
+    }
+    {
+        const float lo = fmaxf(fmaxf(fmaxf(tmin, sx ? rx.y : rx.x), sy ? ry.y : ry.x), sz ? rz.y : rz.x);
+        const float hi = fminf(fminf(fminf(tmax, sx ? rx.x : rx.y), sy ? ry.x : ry.y), sz ? rz.x : rz.y);
+        h.r = SlabHit{!(hi < lo), lo};
+    }
+    return h;
+}
+// Both child boxes of a node record (a, b, q = its first three float4s).
+__device__ __forceinline__ SlabHit slabLeft(float4 a, float4 b, float3 o, float3 inv, float tmin, float tmax) {
+    return slabPair(v2f{a.x, a.y}, v2f{a.z, a.w}, v2f{b.x, b.y}, o, inv, tmin, tmax);
+}
+__device__ __forceinline__ SlabHit slabRight(float4 b, float4 q, float3 o, float3 inv, float tmin, float tmax) {
+    return slabPair(v2f{b.z, b.w}, v2f{q.x, q.y}, v2f{q.z, q.w}, o, inv, tmin, tmax);
 }
 
 // Primitive record (leaf order), 3 x float4:
@@ -261,12 +321,12 @@ __device__ __forceinline__ int trace(const DevScene& S, float3 o, float3 d, floa
         const float4* np = S.nodes + 4 * (size_t)node;
         const float4 a = np[0], b = np[1], q = np[2], r = np[3];
         const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
-        if (slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, closest)) {
+        if (slabLeft(a, b, o, inv, tmin, closest).hit) {
             if (lref & kLeafBit) primTest(S, lref, o, d, tmin, closest, best, c);
             else if (sp < STACK) { stk[sp * kWave] = lref; sp++; }
             else { atomicOr(S.err, 2u); break; }
         }
-        if (slab(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, tmin, closest)) {
+        if (slabRight(b, q, o, inv, tmin, closest).hit) {
             if (rref & kLeafBit) primTest(S, rref, o, d, tmin, closest, best, c);
             else if (sp < STACK) { stk[sp * kWave] = rref; sp++; }
             else { atomicOr(S.err, 2u); break; }
@@ -566,6 +626,13 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 #define PT_LEAF_QUEUE 4
 #endif
 constexpr int kLeafQ = PT_LEAF_QUEUE;
+#ifndef PT_NO_TILE_COST
+#define PT_NO_TILE_COST 0   // diagnostic builds only: no per-tile cost accounting in sample mode
+#endif
+#ifndef PT_TASK_POOL
+#define PT_TASK_POOL 64
+#endif
+constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
 #ifndef PT_WAVES_PER_EU
 #define PT_WAVES_PER_EU 4
 #endif
@@ -598,6 +665,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
 #ifdef PT_DIAG
     uint32_t itN = 0, itL = 0, itS = 0, sPops = 0;   // scheduler diagnostics (iterations per kind)
+    unsigned long long cycN = 0, cycL = 0, cycS = 0;   // and shader cycles per kind
 #define PT_DIAG_ADD(v, x) (v) += (x)
 #else
 #define PT_DIAG_ADD(v, x) ((void)0)
@@ -620,6 +688,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
     uint32_t taskRays = 0, depthPaths = 0;
     bool needTask = SAMPLE;
+    uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode: the wave's reserved tasks (uniform)
 
     // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
     // captured variables address-taken and they end up in scratch memory.)
@@ -644,20 +713,29 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
         }                                                                                         \
     } while (0)
     // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
-    // Sample mode: lanes with needTask take the next tasks of the global counter (one atomic
-    // per wave).  Task t = (tile slot t / 64 / nblocks in launch order, block (t / 64) % nblocks,
-    // pixel t % 64 of the 8x8 tile); tasks off the frame edge are skipped.  Sets `got` for lanes
+    // Sample mode: lanes with needTask take the next tasks of the wave's pool, in lane order; an
+    // empty pool is refilled with the next kTaskPool tasks of the global counter (one returning
+    // atomic, whose latency the wave waits out, per kTaskPool tasks instead of per SHADE step).
+    // Task t = (tile slot t / 64 / nblocks in launch order, block (t / 64) % nblocks, pixel
+    // t % 64 of the 8x8 tile); tasks off the frame edge are skipped.  Sets `got` for lanes
     // that received a task; lanes that find the counter exhausted stop asking.
 #define PT_TAKE_TASKS(got)                                                                          \
     do {                                                                                          \
         for (;;) {                                                                                \
             const uint64_t m_ = __ballot(needTask);                                               \
             if (m_ == 0) break;                                                                   \
-            const int leader_ = __ffsll((unsigned long long)m_) - 1;                              \
-            uint32_t b_ = 0;                                                                      \
-            if (lane == leader_) b_ = atomicAdd(P.taskCounter, (uint32_t)__popcll(m_));           \
+            if (poolLeft == 0u) { /* refill the wave's pool: one returning atomic per kTaskPool */ \
+                const int leader_ = __ffsll((unsigned long long)m_) - 1;                          \
+                uint32_t b_ = 0;                                                                  \
+                if (lane == leader_) b_ = atomicAdd(P.taskCounter, (uint32_t)kTaskPool);          \
+                poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
+                poolLeft = (uint32_t)kTaskPool;                                                   \
+            }                                                                                     \
             /* wave-uniform: the taken tasks span task groups (tile slot, block) g0 and g0 + 1 */ \
-            const uint32_t base_ = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_)); \
+            const uint32_t base_ = poolBase;                                                      \
+            const uint32_t take_ = min((uint32_t)__popcll(m_), poolLeft);                         \
+            poolBase += take_;                                                                    \
+            poolLeft -= take_;                                                                    \
             const uint32_t g0_ = base_ >> 6, off_ = base_ & 63u;                                  \
             const uint32_t slotA_ = g0_ / (uint32_t)P.nblocks, blkA_ = g0_ - slotA_ * (uint32_t)P.nblocks; \
             const bool wrap_ = blkA_ + 1u == (uint32_t)P.nblocks;                                  \
@@ -667,8 +745,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             const uint32_t tB_ = slotB_ < nslots_ ? (P.tileOrder ? (uint32_t)P.tileOrder[slotB_] : slotB_) : 0u; \
             const uint32_t tyA_ = tA_ / (uint32_t)P.tiles_x, txA_ = tA_ - tyA_ * (uint32_t)P.tiles_x; \
             const uint32_t tyB_ = tB_ / (uint32_t)P.tiles_x, txB_ = tB_ - tyB_ * (uint32_t)P.tiles_x; \
-            if (needTask) {                                                                       \
-                const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));             \
+            const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));                 \
+            if (needTask && k_ < take_) {                                                         \
                 if (base_ + k_ >= P.ntasks) {                                                     \
                     needTask = false;                                                             \
                 } else {                                                                          \
@@ -698,7 +776,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
         float* pp_ = P.partial + 3 * ((size_t)blk_ * ((size_t)P.width * (size_t)P.nrows) +        \
                                       (size_t)(r_ * (uint32_t)P.width + c_));                     \
         pp_[0] = sum.x; pp_[1] = sum.y; pp_[2] = sum.z;                                           \
-        atomicAdd(P.tileCost + (r_ >> 3) * (uint32_t)P.tiles_x + (c_ >> 3), taskRays + 1u);       \
+        if (!PT_NO_TILE_COST) atomicAdd(P.tileCost + (r_ >> 3) * (uint32_t)P.tiles_x + (c_ >> 3), taskRays + 1u); \
         needTask = true;                                                                          \
     } while (0)
 #define PT_NEW_PATH()                                                                               \
@@ -766,6 +844,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
         else if (nL >= P.leafBatch) kind = 1;
         else if (nS >= P.shadeBatch) kind = 2;
         else kind = 0;
+#ifdef PT_DIAG
+        const unsigned long long tK0 = __builtin_amdgcn_s_memtime();
+#endif
 
         if (kind == 0) {
             // ------------------------------------------------------------------ NODE
@@ -775,8 +856,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
                 const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
-                const SlabHit hl = slabLo(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, 0.001f, closest);
-                const SlabHit hr = slabLo(b.z, b.w, q.x, q.y, q.z, q.w, o, inv, 0.001f, closest);
+#if PT_PACKED_SLAB
+                SlabHit2 h2 = slabBoth(a, b, q, o, inv, 0.001f, closest);
+                // keep the right child's packed arithmetic next to the left's (not sunk past the
+                // left child's queue append, where the operand pairs are no longer at hand)
+                asm volatile("" : "+v"(h2.r.lo));
+                const SlabHit hl = h2.l, hr = h2.r;
+#else
+                const SlabHit hl = slabLeft(a, b, o, inv, 0.001f, closest);
+                const SlabHit hr = slabRight(b, q, o, inv, 0.001f, closest);
+#endif
                 // append hit leaves in order (left, then right) with their slab entry distances
                 if (hl.hit && (lref & kLeafBit)) {
 #pragma unroll
@@ -890,6 +979,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             sRays += (uint32_t)__popcll(__ballot(newRay));
             sPaths += (uint32_t)__popcll(__ballot(newSample));
         }
+#ifdef PT_DIAG
+        {   // shader-clock cycles per step kind (the step's memory waits included)
+            const unsigned long long dK = __builtin_amdgcn_s_memtime() - tK0;
+            if (kind == 0) cycN += dK;
+            else if (kind == 1) cycL += dK;
+            else cycS += dK;
+        }
+#endif
     }
     if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
         if (valid) {
@@ -920,6 +1017,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
         atomicAdd(P.counters + 9, (unsigned long long)itL);
         atomicAdd(P.counters + 10, (unsigned long long)itS);
         atomicAdd(P.counters + 11, (unsigned long long)sPops);
+        atomicAdd(P.counters + 12, cycN);
+        atomicAdd(P.counters + 13, cycL);
+        atomicAdd(P.counters + 14, cycS);
 #endif
     }
 }
@@ -1077,6 +1177,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void
         else if (nL >= P.leafBatch) kind = 1;
         else if (nS >= P.shadeBatch) kind = 2;
         else kind = 0;
+#ifdef PT_DIAG
+        const unsigned long long tK0 = __builtin_amdgcn_s_memtime();
+#endif
 
         if (kind == 0) {
             // ------------------------------------------------------------------ NODE
@@ -1349,14 +1452,16 @@ __global__ void karrasKernel(const unsigned long long* __restrict__ keys, int n,
 
 // Writes a child box into slot (0 = left, 1 = right) of node p with write-through stores.
 __device__ __forceinline__ void storeBox(float4* nodes, int p, int slot, const float b[6]) {
-    float* f = reinterpret_cast<float*>(nodes + 4 * (size_t)p) + slot * 6;
+    float* f = reinterpret_cast<float*>(nodes + 4 * (size_t)p);
 #pragma unroll
-    for (int i = 0; i < 6; i++) __hip_atomic_store(f + i, b[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 6; i++)   // b = {min xyz, max xyz}
+        __hip_atomic_store(f + nodeBoxIdx(slot, i % 3, i / 3), b[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void loadBox(const float4* nodes, int p, int slot, float b[6]) {
-    const float* f = reinterpret_cast<const float*>(nodes + 4 * (size_t)p) + slot * 6;
+    const float* f = reinterpret_cast<const float*>(nodes + 4 * (size_t)p);
 #pragma unroll
-    for (int i = 0; i < 6; i++) b[i] = __hip_atomic_load(f + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 6; i++)
+        b[i] = __hip_atomic_load(f + nodeBoxIdx(slot, i % 3, i / 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // growBBox (bvh.h:117-130) as a correct bottom-up refit: every leaf writes its box into its
@@ -1647,8 +1752,8 @@ int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
         return r;
     };
     auto boxOf = [&](int n, int slot, float b[6]) {
-        const float* f = reinterpret_cast<const float*>(&bin[4 * (size_t)n]) + 6 * slot;
-        for (int i = 0; i < 6; i++) b[i] = f[i];
+        const float* f = reinterpret_cast<const float*>(&bin[4 * (size_t)n]);
+        for (int i = 0; i < 6; i++) b[i] = f[nodeBoxIdx(slot, i % 3, i / 3)];
     };
     struct Entry { uint32_t ref; bool internal; float box[6]; };
     std::vector<float> out;   // 32 floats per wide node
@@ -2011,12 +2116,12 @@ int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
         out[i].parent = i == 0 ? -1 : iparent[i];
         for (int c = 0; c < 2; c++) {   // child boxes live in this record; copy them to the child
             pt_bvh_node& ch = out[c == 0 ? out[i].left : out[i].right];
-            for (int a = 0; a < 3; a++) { ch.bmin[a] = f[6 * c + a]; ch.bmax[a] = f[6 * c + 3 + a]; }
+            for (int a = 0; a < 3; a++) { ch.bmin[a] = f[nodeBoxIdx(c, a, 0)]; ch.bmax[a] = f[nodeBoxIdx(c, a, 1)]; }
         }
         if (i == 0) {   // the root's own box (never tested by the traversal)
             for (int a = 0; a < 3; a++) {
-                out[0].bmin[a] = std::fmin(f[a], f[6 + a]);
-                out[0].bmax[a] = std::fmax(f[3 + a], f[9 + a]);
+                out[0].bmin[a] = std::fmin(f[nodeBoxIdx(0, a, 0)], f[nodeBoxIdx(1, a, 0)]);
+                out[0].bmax[a] = std::fmax(f[nodeBoxIdx(0, a, 1)], f[nodeBoxIdx(1, a, 1)]);
             }
         }
     }
@@ -2362,6 +2467,11 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         std::fprintf(stderr, "[pt] iterations node %llu leaf %llu shade %llu | lanes/iter node %.1f leaf %.1f "
                      "shade %.1f\n", c[8], c[9], c[10], (double)c[1] / std::max(1ull, c[8]),
                      (double)c[11] / std::max(1ull, c[9]), (double)c[0] / std::max(1ull, c[10]));
+    if (std::getenv("PT_ITER_STATS") && c[12] + c[13] + c[14] > 0)
+        std::fprintf(stderr, "[pt] cycles/iteration node %.0f leaf %.0f shade %.0f | share node %.3f leaf %.3f "
+                     "shade %.3f\n", (double)c[12] / std::max(1ull, c[8]), (double)c[13] / std::max(1ull, c[9]),
+                     (double)c[14] / std::max(1ull, c[10]), (double)c[12] / (double)(c[12] + c[13] + c[14]),
+                     (double)c[13] / (double)(c[12] + c[13] + c[14]), (double)c[14] / (double)(c[12] + c[13] + c[14]));
     if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
     return PT_OK;
 }
