@@ -544,12 +544,16 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
             depthLeft = P.max_depth;
             paths++;
         };
-        // sample mode: close summation block `b` after its last sample
+        // sample mode: close summation block `b` after its last sample (its sum and its ray count,
+        // the tile-cost input of the next launch's longest-first order)
+        uint32_t blockRays0 = 0;
         auto flush = [&]() {
             if constexpr (SAMPLE) {
                 if (sample % P.block == 0 || sample == P.spp) {
-                    float* pp = P.partial + 3 * ((size_t)((sample - 1) / P.block) * ((size_t)P.width * P.nrows) + idx);
-                    pp[0] = sum.x; pp[1] = sum.y; pp[2] = sum.z;
+                    float4* pp = reinterpret_cast<float4*>(P.partial) +
+                                 ((size_t)((sample - 1) / P.block) * ((size_t)P.width * P.nrows) + idx);
+                    *pp = make_float4(sum.x, sum.y, sum.z, __uint_as_float(c.rays - blockRays0 + 1u));
+                    blockRays0 = c.rays;
                     sum = f3(0.0f, 0.0f, 0.0f);
                 }
             }
@@ -596,7 +600,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
         }
     }
-    if (lane == 0) P.tileCost[tile] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - tStart, 0xffffffffull);
+    if (!SAMPLE && lane == 0) P.tileCost[tile] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - tStart, 0xffffffffull);
     waveReduceAdd(P.counters + 0, c.rays);
     waveReduceAdd(P.counters + 1, c.visits);
     waveReduceAdd(P.counters + 2, c.tris);
@@ -626,13 +630,10 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 #define PT_LEAF_QUEUE 4
 #endif
 constexpr int kLeafQ = PT_LEAF_QUEUE;
-#ifndef PT_NO_TILE_COST
-#define PT_NO_TILE_COST 0   // diagnostic builds only: no per-tile cost accounting in sample mode
-#endif
 #ifndef PT_TASK_POOL
 #define PT_TASK_POOL 64
 #endif
-constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
+constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic (64 near the end)
 #ifndef PT_WAVES_PER_EU
 #define PT_WAVES_PER_EU 4
 #endif
@@ -727,9 +728,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             if (poolLeft == 0u) { /* refill the wave's pool: one returning atomic per kTaskPool */ \
                 const int leader_ = __ffsll((unsigned long long)m_) - 1;                          \
                 uint32_t b_ = 0;                                                                  \
-                if (lane == leader_) b_ = atomicAdd(P.taskCounter, (uint32_t)kTaskPool);          \
+                /* large grabs while far from the end, small ones for the tail */                 \
+                const uint32_t grab_ = poolBase + 8u * (uint32_t)kTaskPool * (uint32_t)P.nwaves < P.ntasks \
+                                           ? (uint32_t)kTaskPool : 64u;                           \
+                if (lane == leader_) b_ = atomicAdd(P.taskCounter, grab_);                        \
                 poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
-                poolLeft = (uint32_t)kTaskPool;                                                   \
+                poolLeft = grab_;                                                                 \
             }                                                                                     \
             /* wave-uniform: the taken tasks span task groups (tile slot, block) g0 and g0 + 1 */ \
             const uint32_t base_ = poolBase;                                                      \
@@ -773,10 +777,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     do {                                                                                          \
         const uint32_t blk_ = (uint32_t)(nSamples - 1) / (uint32_t)P.block;                        \
         const uint32_t c_ = cr & 0xffffu, r_ = cr >> 16;                                          \
-        float* pp_ = P.partial + 3 * ((size_t)blk_ * ((size_t)P.width * (size_t)P.nrows) +        \
-                                      (size_t)(r_ * (uint32_t)P.width + c_));                     \
-        pp_[0] = sum.x; pp_[1] = sum.y; pp_[2] = sum.z;                                           \
-        if (!PT_NO_TILE_COST) atomicAdd(P.tileCost + (r_ >> 3) * (uint32_t)P.tiles_x + (c_ >> 3), taskRays + 1u); \
+        float4* pp_ = reinterpret_cast<float4*>(P.partial) +                                      \
+                      ((size_t)blk_ * ((size_t)P.width * (size_t)P.nrows) + (size_t)(r_ * (uint32_t)P.width + c_)); \
+        /* one 16-B store: the block sum and the task's ray count (the tile cost, summed by the \
+           resolve pass; a per-task global atomic here cost 14 % of the frame) */              \
+        *pp_ = make_float4(sum.x, sum.y, sum.z, __uint_as_float(taskRays + 1u));                  \
         needTask = true;                                                                          \
     } while (0)
 #define PT_NEW_PATH()                                                                               \
@@ -1037,8 +1042,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
 // PngImage::saveColor (png_image.h:24-30: (uint8)(clamp(c, 0, 0.999) * 256), alpha 255) or like
 // renderBySurface (main.cu:327-331: (unsigned)(c * 255) into an 8-bit field, alpha 255).
 // Rows stay in film order (row 0 = bottom); the PNG writer flips them.
+// Sample mode: the partials are 16-B records {block sum xyz, rays}; the pixel's rays over all
+// blocks are added to its tile's cost (the next launch's longest-first order).
 __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ src, int nblocks, float* accum,
-                                                     float inv, int format, void* out, int64_t npix) {
+                                                     float inv, int format, void* out, int64_t npix,
+                                                     unsigned* tileCost, int width, int tilesX) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix) return;
     float x, y, z;
@@ -1046,11 +1054,18 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
         x = src[3 * i + 0]; y = src[3 * i + 1]; z = src[3 * i + 2];
     } else {
         x = 0.0f; y = 0.0f; z = 0.0f;
+        uint32_t rays = 0;
+        const float4* q4 = reinterpret_cast<const float4*>(src);
         for (int c = 0; c < nblocks; c++) {
-            const float* q = src + 3 * ((size_t)c * (size_t)npix + (size_t)i);
-            x = x + q[0];
-            y = y + q[1];
-            z = z + q[2];
+            const float4 q = q4[(size_t)c * (size_t)npix + (size_t)i];
+            x = x + q.x;
+            y = y + q.y;
+            z = z + q.z;
+            rays += __float_as_uint(q.w);
+        }
+        if (tileCost) {
+            const int row = (int)(i / width), col = (int)(i - (int64_t)row * width);
+            atomicAdd(tileCost + (row >> 3) * tilesX + (col >> 3), rays);
         }
     }
     if (accum) {
@@ -2366,7 +2381,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
             return fail(PT_ERR_INVALID, "sample mode: frame width and rows must be < 65536");
         P.block = (opts && opts->chunk > 0) ? opts->chunk : std::max(16, (spp + 63) / 64);
         P.nblocks = (spp + P.block - 1) / P.block;
-        const size_t need = (size_t)P.nblocks * (size_t)np * 12;
+        const size_t need = (size_t)P.nblocks * (size_t)np * 16;   // {block sum xyz, rays}
         if (f->partialBytes < need) {
             if ((rc = devAlloc(f->partial, need))) return rc;
             f->partialBytes = need;
@@ -2430,7 +2445,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         resolveKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(sample ? P.partial : f->sums.as<float>(),
                                                                      sample ? P.nblocks : 0,
                                                                      accumulate ? f->accum.as<float>() : nullptr,
-                                                                     inv, fmt, dst, np);
+                                                                     inv, fmt, dst, np,
+                                                                     sample ? f->tileCost.as<unsigned>() : nullptr,
+                                                                     f->width, P.tiles_x);
         HIP_TRY(hipGetLastError());
     }
     if (accumulate) f->accumSamples += spp;
