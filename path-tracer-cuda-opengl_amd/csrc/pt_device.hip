@@ -8,7 +8,8 @@
 //    four dwordx4 loads per visit, one 64-B segment); leaves are folded into the parent's
 //    child refs; the traversal stack lives in LDS, lane-interleaved (conflict-free).
 //  * primitives are stored in Morton (leaf) order, 48 B each ({v0,v1,v2} / {c,r}: the exact
-//    object box is recomputed from them); normals separately (read once per closest hit).
+//    object box is recomputed from them); a 48-B shading record per primitive (normal or
+//    sphere centre/radius + the material inline) is read once per closest hit, in one round trip.
 //  * LBVH: Karras hierarchy kernel + atomic-counter bottom-up refit with tight boxes.
 // All arithmetic follows the reference's operation order and is compiled with
 // -ffp-contract=off, so results are bit-identical to oracle/ (the CPU restatement).
@@ -55,7 +56,7 @@ constexpr int kJumpMats = 32;                    // XORWOW 2^(67+k) jump matrice
 struct DevScene {
     const float4* nodes;     // 4 x float4 per internal node: child boxes as (min, max) pairs per axis, refs (nodeBoxIdx)
     const float4* prims;     // 3 x float4 per primitive (leaf order)
-    const float4* normals;   // 1 x float4 per primitive (triangles)
+    const float4* shade;     // 3 x float4 per primitive: {n | c, r} {albedo, fuzz} {ir, type | sphere << 16, mat, obj}
     const float4* mats;      // 2 x float4 per material
     const float4* wnodes;    // 4-wide nodes, 8 x float4 each (see renderKernelW4)
     unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
@@ -338,24 +339,30 @@ __device__ __forceinline__ int trace(const DevScene& S, float3 o, float3 d, floa
     return best;
 }
 
-// Hit record for leaf slot k at distance t (cuda_object.h:62-67 / 85-88, hit_record.h:21-24).
-struct HitRec { float3 p, n; int mat, obj; bool front; };
+// Hit record for leaf slot k at distance t (cuda_object.h:62-67 / 85-88, hit_record.h:21-24),
+// with the hit object's material (material.h:17-68) carried along: the three independent 16-B
+// loads of the shading record are one memory round trip (instead of prim -> normal -> material).
+struct HitRec { float3 p, n; int mat, obj; bool front; float4 m0; float ir; int type; };
 
 __device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, float3 o, float3 d) {
     HitRec h;
-    const float4* p = S.prims + 3 * (size_t)k;
-    const float4 p0 = p[0], p1 = p[1];
+    const float4* r = S.shade + 3 * (size_t)k;
+    const float4 s0 = r[0], s1 = r[1], s2 = r[2];
+    const uint32_t tf = __float_as_uint(s2.y);
     h.p = add(o, scale(t, d));
     float3 outward;
-    if (__float_as_uint(p[2].w)) {   // sphere
-        outward = divs(sub(h.p, xyz(p0)), p1.x);
+    if (tf >> 16) {   // sphere: (p - c) / r
+        outward = divs(sub(h.p, xyz(s0)), s0.w);
     } else {
-        outward = xyz(S.normals[k]);
+        outward = xyz(s0);
     }
     h.front = dot3(d, outward) < 0.0f;
     h.n = h.front ? outward : neg(outward);
-    h.mat = (int)__float_as_uint(p0.w);
-    h.obj = (int)__float_as_uint(p1.w);
+    h.mat = (int)__float_as_uint(s2.z);
+    h.obj = (int)__float_as_uint(s2.w);
+    h.m0 = s1;
+    h.ir = s2.x;
+    h.type = (int)(tf & 0xffffu);
     return h;
 }
 
@@ -390,8 +397,9 @@ __device__ __forceinline__ float3 reflect3(float3 v, float3 n) { return sub(v, s
 // Material::scatter (material.h:28-61); returns false when the path is absorbed.
 template <class G>
 __device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, float3& d, float3& atten, G& g) {
-    const float4 m0 = S.mats[2 * h.mat], m1 = S.mats[2 * h.mat + 1];
-    const int type = (int)__float_as_uint(m1.y);
+    (void)S;
+    const float4 m0 = h.m0;
+    const int type = h.type;
     if (type == PT_LAMBERTIAN) {
         float3 dir = add(h.n, onUnitSphere(g));
         if (fabsf(dir.x) < 1e-7f && fabsf(dir.y) < 1e-7f && fabsf(dir.z) < 1e-7f) dir = h.n;
@@ -408,7 +416,7 @@ __device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, floa
     }
     if (type == PT_DIELECTRIC) {
         atten = f3(1.0f, 1.0f, 1.0f);
-        const float ir = m1.x;
+        const float ir = h.ir;
         float ratio = h.front ? (1.0f / ir) : ir;
         float3 ud = normalize3(d);
         float cos_t = fminf(dot3(neg(ud), h.n), 1.0f);
@@ -630,6 +638,9 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 #define PT_LEAF_QUEUE 4
 #endif
 constexpr int kLeafQ = PT_LEAF_QUEUE;
+#ifndef PT_LEAF_PREFETCH
+#define PT_LEAF_PREFETCH 1
+#endif
 #ifndef PT_TASK_POOL
 #define PT_TASK_POOL 64
 #endif
@@ -912,6 +923,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             PT_DIAG_ADD(sPops, (uint32_t)nL);
             // Every lane tests all of its queued leaves, in order, in this step (the queue then
             // is empty and the lane rejoins NODE steps; measured -4 % vs one leaf per step).
+            // The first two queued primitives are loaded together up front (their addresses are
+            // known; only the tests depend on `closest`): one memory round trip for two leaves.
+#if PT_LEAF_PREFETCH
+            Prim pf0{}, pf1{};
+            if (qn > 0) pf0 = loadPrim(S, qref[0] & kPrimMask);
+            if (qn > 1) pf1 = loadPrim(S, qref[1] & kPrimMask);
+#endif
+#pragma unroll
             for (int k_ = 0; k_ < kLeafQ; k_++) {
                 const bool act = qn > 0;
                 if (__ballot(act) == 0) break;
@@ -929,7 +948,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 // was queued, with a tmax >= closest, so now it fails iff closest < lo (slabLo).
                 if (!(closest < lo)) {
                     tested = true;
-                    const float t = primHitT(loadPrim(S, k), sph, o, d, 0.001f, closest);
+#if PT_LEAF_PREFETCH
+                    const Prim pr = k_ == 0 ? pf0 : (k_ == 1 ? pf1 : loadPrim(S, k));
+#else
+                    const Prim pr = loadPrim(S, k);
+#endif
+                    const float t = primHitT(pr, sph, o, d, 0.001f, closest);
                     if (t >= 0.0f) { closest = t; best = (int)k; }
                 }
             }
@@ -1605,8 +1629,9 @@ __global__ __launch_bounds__(256) void mortonKernel(const pt_object* __restrict_
 __global__ __launch_bounds__(256) void leafGatherKernel(const pt_object* __restrict__ objs,
                                                         const uint32_t* __restrict__ codes,
                                                         const uint32_t* __restrict__ ids, int64_t n,
-                                                        unsigned long long* keys, float4* prims, float4* normals,
-                                                        float* boxes, uint32_t* sphereFlag) {
+                                                        unsigned long long* keys, float4* prims, float4* shade,
+                                                        float* boxes, uint32_t* sphereFlag,
+                                                        const float4* __restrict__ mats) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t id = ids[k];
@@ -1619,7 +1644,7 @@ __global__ __launch_bounds__(256) void leafGatherKernel(const pt_object* __restr
         prims[3 * k] = make_float4(o.v[0], o.v[1], o.v[2], __uint_as_float((uint32_t)o.mat));
         prims[3 * k + 1] = make_float4(o.v[3], 0.0f, 0.0f, __uint_as_float(id));
         prims[3 * k + 2] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(1u));
-        normals[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        shade[3 * k] = make_float4(o.v[0], o.v[1], o.v[2], o.v[3]);
         sphereFlag[k] = 1u;
     } else {
         const float3 v0 = f3(o.v[0], o.v[1], o.v[2]), v1 = f3(o.v[3], o.v[4], o.v[5]), v2 = f3(o.v[6], o.v[7], o.v[8]);
@@ -1627,9 +1652,14 @@ __global__ __launch_bounds__(256) void leafGatherKernel(const pt_object* __restr
         prims[3 * k] = make_float4(v0.x, v0.y, v0.z, __uint_as_float((uint32_t)o.mat));
         prims[3 * k + 1] = make_float4(v1.x, v1.y, v1.z, __uint_as_float(id));
         prims[3 * k + 2] = make_float4(v2.x, v2.y, v2.z, 0.0f);
-        normals[k] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+        shade[3 * k] = make_float4(nn.x, nn.y, nn.z, 0.0f);
         sphereFlag[k] = 0u;
     }
+    // the object's material inline: {albedo, fuzz}, {ir, type | sphere << 16, mat, obj}
+    const float4 m0 = mats[2 * o.mat], m1 = mats[2 * o.mat + 1];
+    shade[3 * k + 1] = m0;
+    shade[3 * k + 2] = make_float4(m1.x, __uint_as_float(__float_as_uint(m1.y) | (o.type == PT_SPHERE ? 0x10000u : 0u)),
+                                   __uint_as_float((uint32_t)o.mat), __uint_as_float(id));
 }
 
 // Depth of the internal hierarchy (root = 1) = the most internal ancestors of any leaf.
@@ -1725,7 +1755,7 @@ struct pt_scene {
     int64_t nobj = 0, nmat = 0;
     std::vector<pt_object> objs;            // host copy (PT_BVH_HOST_KEYS path)
     DevBuf dobjs;                           // the objects on the device (BVH build input)
-    DevBuf mats, nodes, prims, normals, counters;
+    DevBuf mats, nodes, prims, shade, counters;
     DevBuf keys, iparent, lparent, leafBoxes;   // sorted 64-bit Morton keys, parent links, leaf boxes
     DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelW4), built on first use
     int wideDepth = 0;
@@ -1912,7 +1942,7 @@ DevScene devScene(const pt_scene* s) {
     DevScene S;
     S.nodes = s->nodes.as<float4>();
     S.prims = s->prims.as<float4>();
-    S.normals = s->normals.as<float4>();
+    S.shade = s->shade.as<float4>();
     S.mats = s->mats.as<float4>();
     S.wnodes = s->wide.as<float4>();
     S.err = reinterpret_cast<unsigned int*>(s->counters.as<unsigned long long>() + 7);
@@ -1993,7 +2023,7 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     // leaf records -> Karras hierarchy -> refit -> depth.  (PT_BVH_HOST_KEYS: the keys come from
     // the host restatement of computeMortonOnHost instead; the result is identical.)
     const size_t n1 = (size_t)std::max<int64_t>(1, n), ni = (size_t)std::max<int64_t>(1, n - 1);
-    if ((rc = devAlloc(s->prims, n1 * 3 * sizeof(float4))) || (rc = devAlloc(s->normals, n1 * sizeof(float4))) ||
+    if ((rc = devAlloc(s->prims, n1 * 3 * sizeof(float4))) || (rc = devAlloc(s->shade, n1 * 3 * sizeof(float4))) ||
         (rc = devAlloc(s->nodes, ni * 4 * sizeof(float4))) || (rc = devAlloc(s->keys, n1 * 8)) ||
         (rc = devAlloc(s->leafBoxes, n1 * 24)) || (rc = devAlloc(s->iparent, ni * 4)) ||
         (rc = devAlloc(s->lparent, n1 * 4)))
@@ -2033,7 +2063,8 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
         }
         leafGatherKernel<<<nb, tb, 0, st>>>(s->dobjs.as<pt_object>(), codes2.as<uint32_t>(), ids2.as<uint32_t>(), n,
                                             s->keys.as<unsigned long long>(), s->prims.as<float4>(),
-                                            s->normals.as<float4>(), s->leafBoxes.as<float>(), sph.as<uint32_t>());
+                                            s->shade.as<float4>(), s->leafBoxes.as<float>(), sph.as<uint32_t>(),
+                                            s->mats.as<float4>());
         HIP_TRY(hipGetLastError());
     }
     HIP_TRY(hipMemsetAsync(s->nodes.p, 0, ni * 4 * sizeof(float4), st));
@@ -2062,7 +2093,7 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     HIP_TRY(hipMemcpy(&depth, dep.p, 4, hipMemcpyDeviceToHost));
     s->depth = n > 1 ? depth : 0;
     if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
-    s->deviceBytes = (size_t)(n > 1 ? n - 1 : 0) * 64 + (size_t)n * 64 + (size_t)s->nmat * 32;
+    s->deviceBytes = (size_t)(n > 1 ? n - 1 : 0) * 64 + (size_t)n * 96 + (size_t)s->nmat * 32;
     s->built = true;
     return PT_OK;
 }
