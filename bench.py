@@ -248,6 +248,9 @@ def main() -> None:
                          "algo_bytes_per_launch": kbytes / args.steps,
                          "algo_bytes_source": "reference-order traversal counts of the same frame "
                                               "(ray-synchronous kernel, warmup step 1)",
+                         "note": "algorithmic bytes (SURVEY 8(d): 56 B/node visit + 40 B/triangle test) consumed "
+                                 "per kernel second; the BVH is cache-resident (L2 for C2/C3), so frac can "
+                                 "exceed 1 -- HBM bytes actually moved per launch are `traffic` (PMC)",
                          "node_visits_reference": ref_st.node_visits,
                          "node_visits_wavefront": spec_visits / args.steps},
         }

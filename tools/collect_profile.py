@@ -33,7 +33,7 @@ def main(tag):
             open(os.path.join(dst, "kernel_trace_render.csv"), "w") as g:
         lines = f.readlines()
         g.write(lines[0])
-        g.writelines(l for l in lines[1:] if "render" in l or "reduceChunks" in l)
+        g.writelines(l for l in lines[1:] if "render" in l or "resolve" in l)
     for p in ("fetch", "write", "tcc", "sq"):
         shutil.copy(os.path.join(src, f"pmc_{p}", "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
 
