@@ -58,7 +58,7 @@ struct DevScene {
     const float4* prims;     // 3 x float4 per primitive (leaf order)
     const float4* shade;     // 3 x float4 per primitive: {n | c, r} {albedo, fuzz} {ir, type | sphere << 16, mat, obj}
     const float4* mats;      // 2 x float4 per material
-    const float4* wnodes;    // 4-wide nodes, 8 x float4 each (see renderKernelW4)
+    const float4* wnodes;    // 4-wide nodes, 8 x float4 each (renderKernelWF<.., WIDE>)
     unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
     int nprims;
 };
@@ -638,6 +638,9 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 #define PT_LEAF_QUEUE 4
 #endif
 constexpr int kLeafQ = PT_LEAF_QUEUE;
+#ifndef PT_WIDE_EXACT
+#define PT_WIDE_EXACT 0   // debug: re-test every wide-tree leaf from its vertices
+#endif
 #ifndef PT_LEAF_PREFETCH
 #define PT_LEAF_PREFETCH 1
 #endif
@@ -649,7 +652,101 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 #define PT_WAVES_PER_EU 4
 #endif
 
-template <int STACK, bool SAMPLE>
+// One NODE step on the 4-wide tree for one lane.  Entries of a wide node are in the reference's
+// DFS order: leading hit leaves go to the leaf queue (with their entry distance), the first hit
+// internal entry is visited next, the hit entries after it are pushed in reverse order; with no
+// internal entry to descend into, stack tops are popped (leaves into the queue) until an internal
+// node, an empty stack or a full queue (node = -2: continue when the queue has room).
+template <int STACK>
+__device__ __forceinline__ void wideNodeStep(const DevScene& S, int& node, int& sp, int& qn, uint32_t (&qref)[kLeafQ],
+                                             float (&lq)[kLeafQ], uint32_t* my, float3 o, float3 inv,
+                                             float closest) {
+    bool needPop = node == -2;
+    if (node >= 0) {
+        const float4* np = S.wnodes + 8 * (size_t)node;
+        const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
+        const float4 rf = np[6];
+        const SlabHit h0 = slabLo(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, 0.001f, closest);
+        const SlabHit h1 = slabLo(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, 0.001f, closest);
+        const SlabHit h2 = slabLo(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, 0.001f, closest);
+        const SlabHit h3 = slabLo(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, 0.001f, closest);
+        int mask = (h0.hit ? 1 : 0) | (h1.hit ? 2 : 0) | (h2.hit ? 4 : 0) | (h3.hit ? 8 : 0);
+        const uint32_t refs[4] = {__float_as_uint(rf.x), __float_as_uint(rf.y), __float_as_uint(rf.z),
+                                  __float_as_uint(rf.w)};
+        const float los[4] = {h0.lo, h1.lo, h2.lo, h3.lo};
+        int next = -1;
+        bool full = false;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            if (next < 0 && !full && ((mask >> e) & 1)) {
+                const uint32_t ref = refs[e];
+                if (ref & kLeafBit) {
+                    if (qn < kLeafQ) {
+#pragma unroll
+                        for (int i = 0; i < kLeafQ; i++) {
+                            qref[i] = qn == i ? ref : qref[i];
+                            lq[i] = qn == i ? (PT_WIDE_EXACT ? -__builtin_inff() : los[e]) : lq[i];
+                        }
+                        qn++;
+                        mask &= ~(1 << e);
+                    } else {
+                        full = true;
+                    }
+                } else {
+                    next = (int)ref;
+                    mask &= ~(1 << e);
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 3; e >= 0; e--) {
+            if ((mask >> e) & 1) {
+                if (sp < STACK) { my[sp * kWave] = refs[e]; sp++; }
+                else { atomicOr(S.err, 2u); }
+            }
+        }
+        if (next >= 0) node = next;
+        else if (full) node = -2;
+        else needPop = true;
+    }
+    if (needPop) {   // pop stacked leaves into the queue until an internal node (bounded)
+        node = -1;
+        bool decided = false;
+#pragma unroll
+        for (int it = 0; it < 4; it++) {
+            if (!decided) {
+                if (sp == 0) {
+                    decided = true;
+                } else {
+                    const uint32_t e = my[(sp - 1) * kWave];
+                    if (!(e & kLeafBit)) {
+                        node = (int)e;
+                        sp--;
+                        decided = true;
+                    } else if (qn < kLeafQ) {
+#pragma unroll
+                        for (int i = 0; i < kLeafQ; i++) {
+                            qref[i] = qn == i ? e : qref[i];
+                            lq[i] = qn == i ? -__builtin_inff() : lq[i];
+                        }
+                        qn++;
+                        sp--;
+                    } else {
+                        node = -2;
+                        decided = true;
+                    }
+                }
+            }
+        }
+        if (!decided) node = sp > 0 ? -2 : -1;
+    }
+}
+
+// WIDE: traverse the 4-wide collapse of the LBVH (wnodes; layout and entry order above traceKernel);
+// a ray needs about half the dependent NODE steps.  Leaves reached directly are queued with their
+// slab entry distance; leaves that wait on the stack behind an internal entry are queued with
+// lo = -inf and re-tested exactly from the primitive's vertices (primBoxHit).
+template <int STACK, bool SAMPLE, bool WIDE>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
@@ -849,9 +946,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
               (!SAMPLE && P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
 
     for (;;) {
-        const bool wantNode = node >= 0 && qn <= kLeafQ - 2;
+        // binary: room for both children's leaves; wide: a node (the step handles a full queue)
+        // or a stack top waiting for queue space (node == -2)
+        const bool wantNode = WIDE ? (node >= 0 || (node == -2 && qn < kLeafQ)) : (node >= 0 && qn <= kLeafQ - 2);
         const bool wantLeaf = qn > 0;
-        const bool wantShade = (active && node < 0 && qn == 0) || needTask;
+        const bool wantShade = (active && node == -1 && qn == 0) || needTask;   // (-2: wide stack top pending)
         const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
@@ -868,7 +967,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             // ------------------------------------------------------------------ NODE
             sVisits += (uint32_t)nN;
             PT_DIAG_ADD(itN, 1u);
-            if (wantNode) {
+            if constexpr (WIDE) {
+                if (wantNode) wideNodeStep<STACK>(S, node, sp, qn, qref, lq, my, o, inv, closest);
+            } else if (wantNode) {
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
                 const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
@@ -947,14 +1048,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 // Exact re-test of the leaf box with the current closest: the box passed when it
                 // was queued, with a tmax >= closest, so now it fails iff closest < lo (slabLo).
                 if (!(closest < lo)) {
-                    tested = true;
 #if PT_LEAF_PREFETCH
                     const Prim pr = k_ == 0 ? pf0 : (k_ == 1 ? pf1 : loadPrim(S, k));
 #else
                     const Prim pr = loadPrim(S, k);
 #endif
-                    const float t = primHitT(pr, sph, o, d, 0.001f, closest);
-                    if (t >= 0.0f) { closest = t; best = (int)k; }
+                    // (wide: a leaf that waited on the stack has no entry distance, lo = -inf:
+                    // exact re-test of its box from the primitive's vertices)
+                    if (!(WIDE && lo == -__builtin_inff()) || primBoxHit(pr, sph, o, inv, 0.001f, closest)) {
+                        tested = true;
+                        const float t = primHitT(pr, sph, o, d, 0.001f, closest);
+                        if (t >= 0.0f) { closest = t; best = (int)k; }
+                    }
                 }
             }
             sTris += (uint32_t)__popcll(__ballot(tested && !sph));
@@ -1119,7 +1224,7 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
     static_cast<uint32_t*>(out)[i] = px;
 }
 
-// 4-wide variant of renderKernelWF.  Wide node (128 B = 8 x float4): SoA child boxes
+// The 4-wide tree (renderKernelWF<.., WIDE = true>).  Wide node (128 B = 8 x float4): SoA child boxes
 // {minx[4]}{miny[4]}{minz[4]}{maxx[4]}{maxy[4]}{maxz[4]}, {ref[4]}, pad.  A wide node is a
 // two-level collapse of the reference LBVH node N whose entries are listed in the reference's
 // DFS order: [L if leaf][R if leaf] + expand(R) + expand(L), expand(X) = [XL if leaf][XR if
@@ -1127,256 +1232,6 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
 // skipped binary ancestor's is exact (the entry box is inside the ancestor box: the slab
 // interval can only shrink), and leaves keep the exact re-test, so every pixel is identical to
 // the reference order; a ray needs about half the dependent node steps.
-template <int STACK>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(5))) void renderKernelW4(RenderParams P) {
-    __shared__ uint32_t stk[STACK * kWave];
-    const int lane = threadIdx.x;
-    const int tile = tileOf(P, blockIdx.x);
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    const int col = tx * 8 + (lane & 7);
-    const int lrow = ty * 8 + (lane >> 3);
-    const bool valid = col < P.width && lrow < P.nrows;
-    const size_t idx = valid ? (size_t)lrow * P.width + col : 0;
-    const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
-    if ((int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
-    const float fcol = (float)col;
-    const float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
-    const DevScene& S = P.S;
-    uint32_t* my = stk + lane;
-    // Work counters are wave totals kept in scalar registers: each step adds the popcount of
-    // a ballot of the lanes that did the work (no per-lane counter VGPRs).
-    uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
-
-    Xorwow g{0, 0, 0, 0, 0, 0};
-    if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
-    float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
-    float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
-    float closest = 0.0f;
-    int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
-    // node >= 0: wide node to visit; -2: the stack top must be popped (a leaf waiting for queue
-    // space); -1: traversal of the current ray complete
-    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // leaf queue: leaf refs in DFS order
-    bool active = false;
-
-    // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
-    // captured variables address-taken and they end up in scratch memory.)
-#define PT_BEGIN_RAY()                                                                              \
-    do {                                                                                          \
-        depthLeft--;                                                                              \
-        closest = __builtin_inff();                                                               \
-        best = -1;                                                                                \
-        sp = 0;                                                                                   \
-        qn = 0;                                                                                   \
-        if (S.nprims <= 1) {                                                                      \
-            node = -1;                                                                            \
-            if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
-                const float t1 = primHitT(loadPrim(S, 0), __float_as_uint(S.prims[2].w) != 0, o, d, \
-                                          0.001f, closest);                                       \
-                if (t1 >= 0.0f) { closest = t1; best = 0; }                                       \
-            }                                                                                     \
-        } else {                                                                                  \
-            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
-            node = 0;                                                                             \
-        }                                                                                         \
-    } while (0)
-    // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
-#define PT_NEW_PATH()                                                                               \
-    do {                                                                                          \
-        const float u_ = (fcol + g.uniform()) * P.invW;                                           \
-        const float v_ = (frow + g.uniform()) * P.invH;                                           \
-        o = P.cam.pos;                                                                            \
-        d = sub(add(add(P.cam.ll, scale(u_, P.cam.hor)), scale(v_, P.cam.ver)), P.cam.pos);       \
-        att = f3(1.0f, 1.0f, 1.0f);                                                               \
-        depthLeft = P.max_depth;                                                                  \
-    } while (0)
-
-    bool started = false;
-    if (valid) {
-        if (P.max_depth <= 0) {
-            for (; sample < P.spp; sample++) { PT_NEW_PATH(); sum = add(sum, sky(d, att)); }
-        } else if (P.spp > 0) {
-            PT_NEW_PATH();
-            PT_BEGIN_RAY();
-            active = true;
-            started = true;
-        }
-    }
-    sRays += (uint32_t)__popcll(__ballot(started));
-    sPaths += (uint32_t)__popcll(__ballot(started)) + (P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)P.spp : 0u);
-
-    for (;;) {
-        const bool wantNode = node >= 0 || (node == -2 && qn < kLeafQ);
-        const bool wantLeaf = qn > 0;
-        const bool wantShade = active && node == -1 && qn == 0;
-        const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
-        if ((mN | mL | mS) == 0) break;
-        const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
-        int kind;   // 0 node, 1 leaf, 2 shade
-        if (nN == 0) kind = nL > 0 ? 1 : 2;
-        else if (nL >= P.leafBatch) kind = 1;
-        else if (nS >= P.shadeBatch) kind = 2;
-        else kind = 0;
-#ifdef PT_DIAG
-        const unsigned long long tK0 = __builtin_amdgcn_s_memtime();
-#endif
-
-        if (kind == 0) {
-            // ------------------------------------------------------------------ NODE
-            sVisits += (uint32_t)nN;
-            if (wantNode) {
-                bool needPop = node == -2;
-                if (node >= 0) {
-                    const float4* np = S.wnodes + 8 * (size_t)node;
-                    const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
-                    const float4 rf = np[6];
-                    int mask = (slab(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, 0.001f, closest) ? 1 : 0) |
-                               (slab(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, 0.001f, closest) ? 2 : 0) |
-                               (slab(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, 0.001f, closest) ? 4 : 0) |
-                               (slab(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, 0.001f, closest) ? 8 : 0);
-                    const uint32_t refs[4] = {__float_as_uint(rf.x), __float_as_uint(rf.y), __float_as_uint(rf.z),
-                                              __float_as_uint(rf.w)};
-                    // Entries are in the reference's DFS order.  Leading hit leaves go straight to
-                    // the leaf queue, the first hit internal entry is visited next, and the hit
-                    // entries after it are pushed individually in reverse order.
-                    int next = -1;
-                    bool full = false;
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        if (next < 0 && !full && ((mask >> e) & 1)) {
-                            const uint32_t ref = refs[e];
-                            if (ref & kLeafBit) {
-                                if (qn < kLeafQ) {
-                                    q0 = qn == 0 ? ref : q0; q1 = qn == 1 ? ref : q1; q2 = qn == 2 ? ref : q2; q3 = qn == 3 ? ref : q3;
-                                    qn++;
-                                    mask &= ~(1 << e);
-                                } else {
-                                    full = true;
-                                }
-                            } else {
-                                next = (int)ref;
-                                mask &= ~(1 << e);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int e = 3; e >= 0; e--) {
-                        if ((mask >> e) & 1) {
-                            if (sp < STACK) { my[sp * kWave] = refs[e]; sp++; }
-                            else { atomicOr(S.err, 2u); }
-                        }
-                    }
-                    if (next >= 0) node = next;
-                    else if (full) node = -2;
-                    else needPop = true;
-                }
-                if (needPop) {   // pop queued leaves until an internal node (bounded)
-                    node = -1;
-                    bool decided = false;
-#pragma unroll
-                    for (int it = 0; it < 4; it++) {
-                        if (!decided) {
-                            if (sp == 0) {
-                                decided = true;
-                            } else {
-                                const uint32_t e = my[(sp - 1) * kWave];
-                                if (!(e & kLeafBit)) {
-                                    node = (int)e;
-                                    sp--;
-                                    decided = true;
-                                } else if (qn < kLeafQ) {
-                                    q0 = qn == 0 ? e : q0; q1 = qn == 1 ? e : q1; q2 = qn == 2 ? e : q2; q3 = qn == 3 ? e : q3;
-                                    qn++;
-                                    sp--;
-                                } else {
-                                    node = -2;
-                                    decided = true;
-                                }
-                            }
-                        }
-                    }
-                    if (!decided) node = sp > 0 ? -2 : -1;
-                }
-            }
-        } else if (kind == 1) {
-            // ------------------------------------------------------------------ LEAF
-            bool tested = false, sph = false;
-            if (wantLeaf) {
-                const uint32_t ref = q0;
-                q0 = q1; q1 = q2; q2 = q3;
-                qn--;
-                const uint32_t k = ref & kPrimMask;
-                sph = (ref & kSphereBit) != 0;
-                const Prim pr = loadPrim(S, k);
-                if (primBoxHit(pr, sph, o, inv, 0.001f, closest)) {
-                    tested = true;
-                    const float t = primHitT(pr, sph, o, d, 0.001f, closest);
-                    if (t >= 0.0f) { closest = t; best = (int)k; }
-                }
-            }
-            sTris += (uint32_t)__popcll(__ballot(tested && !sph));
-            sSph += (uint32_t)__popcll(__ballot(tested && sph));
-        } else {
-            // ------------------------------------------------------------------ SHADE
-            bool newRay = false, newSample = false;
-            if (wantShade) {
-                bool done = false;
-                float3 contrib = f3(0.0f, 0.0f, 0.0f);
-                if (best < 0) {
-                    contrib = sky(d, att);
-                    done = true;
-                } else {
-                    HitRec h = makeHit(S, best, closest, o, d);
-                    float3 na;
-                    if (!scatter(S, h, d, na, g)) {
-                        done = true;
-                    } else {
-                        att = mul(att, na);
-                        o = h.p;
-                        if (depthLeft == 0) { contrib = sky(d, att); done = true; }
-                    }
-                }
-                if (done) {
-                    sum = add(sum, contrib);
-                    if (++sample == P.spp) {
-                        active = false;
-                    } else {
-                        PT_NEW_PATH();
-                        PT_BEGIN_RAY();
-                        newRay = newSample = true;
-                    }
-                } else {
-                    PT_BEGIN_RAY();
-                    newRay = true;
-                }
-            }
-            sRays += (uint32_t)__popcll(__ballot(newRay));
-            sPaths += (uint32_t)__popcll(__ballot(newSample));
-        }
-    }
-    if (valid) {
-        storePixel(P, idx, sum);
-        P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
-    }
-    const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
-    if (P.waveTimes && lane == 0) {
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        P.waveTimes[3 * (size_t)blockIdx.x + 0] = tStart;
-        P.waveTimes[3 * (size_t)blockIdx.x + 1] = tEnd;
-        P.waveTimes[3 * (size_t)blockIdx.x + 2] = (unsigned long long)tile | ((unsigned long long)(xcc & 0xf) << 32);
-    }
-    if (lane == 0) {
-        atomicAdd(P.counters + 0, (unsigned long long)sRays);
-        atomicAdd(P.counters + 1, (unsigned long long)sVisits);
-        atomicAdd(P.counters + 2, (unsigned long long)sTris);
-        atomicAdd(P.counters + 3, (unsigned long long)sSph);
-        atomicAdd(P.counters + 4, (unsigned long long)sPaths);
-    }
-}
-#undef PT_BEGIN_RAY
-#undef PT_NEW_PATH
-
 template <int STACK>
 __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* rays, int64_t n, float tmin,
                                                      float tmax, pt_hit* hits, unsigned long long* counters) {
@@ -1757,7 +1612,7 @@ struct pt_scene {
     DevBuf dobjs;                           // the objects on the device (BVH build input)
     DevBuf mats, nodes, prims, shade, counters;
     DevBuf keys, iparent, lparent, leafBoxes;   // sorted 64-bit Morton keys, parent links, leaf boxes
-    DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelW4), built on first use
+    DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelWF<.., WIDE>), built on first use
     int wideDepth = 0;
     int64_t wideNodes = 0;
     int depth = 0;
@@ -1788,7 +1643,7 @@ struct pt_film {
 
 namespace {
 // Collapse the binary LBVH (device records downloaded into `bin`) into 4-wide nodes whose
-// entries follow the reference's DFS order (see renderKernelW4).
+// entries follow the reference's DFS order (renderKernelWF<.., WIDE>).
 int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
     auto refOf = [&](int n, int slot) {
         float f = slot == 0 ? bin[4 * (size_t)n + 3].x : bin[4 * (size_t)n + 3].y;
@@ -1857,7 +1712,7 @@ int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
         for (int k = 28; k < 32; k++) W[k] = 0.0f;
         nent[w] = (int)e.size();
     }
-    // Worst-case stack use of renderKernelW4 (every entry hit): a visit pushes at most
+    // Worst-case stack use of the wide traversal (every entry hit): a visit pushes at most
     // entries-1 items, then one subtree below it is active.  Children have larger indices.
     std::vector<int> need(nent.size(), 0);
     for (size_t w = nent.size(); w-- > 0;) {
@@ -1886,10 +1741,11 @@ int setDevice(int dev) {
 
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
-    if (P.kernel == PT_KERNEL_WIDE) renderKernelW4<S><<<P.ntiles, kWave, 0, st>>>(P);
+    if (P.kernel == PT_KERNEL_WIDE && P.partial) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WIDE) renderKernelWF<S, false, true><<<P.ntiles, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
-        renderKernelWF<S, true><<<P.nwaves, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false><<<P.ntiles, kWave, 0, st>>>(P);
+        renderKernelWF<S, true, false><<<P.nwaves, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false, false><<<P.ntiles, kWave, 0, st>>>(P);
     else if (P.partial) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
@@ -2370,11 +2226,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
 
     const int rng = opts ? opts->rng : PT_RNG_COMPAT;
     if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
-    if (rng == PT_RNG_SAMPLE && kernel == PT_KERNEL_WIDE) {
-        if (opts && opts->kernel != PT_KERNEL_DEFAULT)
-            return fail(PT_ERR_INVALID, "pt_render_ex: sample mode runs on the wavefront or simple kernel");
-        kernel = PT_KERNEL_WAVEFRONT;
-    }
+
     if (kernel == PT_KERNEL_WIDE) {
         if ((rc = ensureWide(s))) return rc;
         P.S = devScene(s);   // now with the wide nodes

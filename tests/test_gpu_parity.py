@@ -352,6 +352,13 @@ def test_sample_mode_bit_exact(pt, orc, gpu, name, w, h, spp, depth, chunk, monk
     srgb, sst = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk, kernel=pt.KERNEL_SIMPLE)
     np.testing.assert_array_equal(bits(srgb), bits(ref))
     assert sst.node_visits == rst.node_visits and sst.tri_tests == rst.tri_tests
+    # the 4-wide tree: same frame, same primitive tests (the reference's order)
+    for leaf, shade in (("24", "32"), ("1", "1")):
+        monkeypatch.setenv("PT_LEAF_BATCH", leaf)
+        monkeypatch.setenv("PT_SHADE_BATCH", shade)
+        wrgb, wst = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk, kernel=pt.KERNEL_WIDE)
+        np.testing.assert_array_equal(bits(wrgb), bits(ref))
+        assert wst.rays == rst.rays and wst.tri_tests == rst.tri_tests and wst.sphere_tests == rst.sphere_tests
 
 
 def test_sample_mode_stateless_and_stripes(pt, orc, gpu):
@@ -387,11 +394,13 @@ def test_sample_mode_options(pt, gpu):
     f = pt.Film(16, 16, 1, device=gpu)
     with pytest.raises(pt.PtError):
         pt.render(s, f, p.camera, 1, 5, rng=5)
-    with pytest.raises(pt.PtError):   # sample mode runs on the wavefront and simple kernels
-        pt.render(s, f, p.camera, 1, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WIDE)
+    with pytest.raises(pt.PtError):
+        pt.render(s, f, p.camera, 1, 5, rng=pt.RNG_SAMPLE, kernel=9)
     a, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WAVEFRONT)
     b, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE)
+    c, _ = pt.render(s, f, p.camera, 2, 5, rng=pt.RNG_SAMPLE, kernel=pt.KERNEL_WIDE)
     np.testing.assert_array_equal(bits(a), bits(b))
+    np.testing.assert_array_equal(bits(a), bits(c))
     _, st = pt.render(s, f, p.camera, 2, 0, rng=pt.RNG_SAMPLE)   # depth 0: no rays traced
     assert st.rays == 0
 

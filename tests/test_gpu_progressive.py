@@ -48,10 +48,10 @@ def test_accumulate_compat_matches_oracle(pt, orc, setup):
     np.testing.assert_array_equal(film.get_rng(), states)
 
 
-@pytest.mark.parametrize("kernel", ["wavefront", "simple"])
+@pytest.mark.parametrize("kernel", ["wavefront", "simple", "wide"])
 def test_accumulate_sample_matches_oracle(pt, orc, setup, kernel):
     p, scene, nodes, cam = setup
-    k = pt.KERNEL_WAVEFRONT if kernel == "wavefront" else pt.KERNEL_SIMPLE
+    k = {"wavefront": pt.KERNEL_WAVEFRONT, "simple": pt.KERNEL_SIMPLE, "wide": pt.KERNEL_WIDE}[kernel]
     film = pt.Film(W, H, seed=9)
     spps, chunk = [3, 5, 2], 2
     sums, base = [], 0
