@@ -638,6 +638,9 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 #define PT_LEAF_QUEUE 4
 #endif
 constexpr int kLeafQ = PT_LEAF_QUEUE;
+#ifndef PT_LEAF_QUEUE_SAMPLE
+#define PT_LEAF_QUEUE_SAMPLE 2   // sample mode, binary tree: 1067 vs 1088 ms (depth 4); compat prefers 4 (1774 vs 1959)
+#endif
 #ifndef PT_WIDE_EXACT
 #define PT_WIDE_EXACT 0   // debug: re-test every wide-tree leaf from its vertices
 #endif
@@ -789,10 +792,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
     int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
-    uint32_t qref[kLeafQ];   // leaf queue: leaf refs in DFS order (registers: constant indices only)
-    float lq[kLeafQ];     // their slab entry distances
+    constexpr int LQ = (SAMPLE && !WIDE) ? PT_LEAF_QUEUE_SAMPLE : kLeafQ;   // leaf queue depth
+    uint32_t qref[LQ];   // leaf queue: leaf refs in DFS order (registers: constant indices only)
+    float lq[LQ];     // their slab entry distances
 #pragma unroll
-    for (int i = 0; i < kLeafQ; i++) { qref[i] = 0u; lq[i] = 0.0f; }
+    for (int i = 0; i < LQ; i++) { qref[i] = 0u; lq[i] = 0.0f; }
     bool active = false;
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
     uint32_t taskRays = 0, depthPaths = 0;
@@ -948,7 +952,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     for (;;) {
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
-        const bool wantNode = WIDE ? (node >= 0 || (node == -2 && qn < kLeafQ)) : (node >= 0 && qn <= kLeafQ - 2);
+        const bool wantNode = WIDE ? (node >= 0 || (node == -2 && qn < LQ)) : (node >= 0 && qn <= LQ - 2);
         const bool wantLeaf = qn > 0;
         const bool wantShade = (active && node == -1 && qn == 0) || needTask;   // (-2: wide stack top pending)
         const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
@@ -986,7 +990,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 // append hit leaves in order (left, then right) with their slab entry distances
                 if (hl.hit && (lref & kLeafBit)) {
 #pragma unroll
-                    for (int i = 0; i < kLeafQ; i++) {
+                    for (int i = 0; i < LQ; i++) {
                         qref[i] = qn == i ? lref : qref[i];
                         lq[i] = qn == i ? hl.lo : lq[i];
                     }
@@ -994,7 +998,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 }
                 if (hr.hit && (rref & kLeafBit)) {
 #pragma unroll
-                    for (int i = 0; i < kLeafQ; i++) {
+                    for (int i = 0; i < LQ; i++) {
                         qref[i] = qn == i ? rref : qref[i];
                         lq[i] = qn == i ? hr.lo : lq[i];
                     }
@@ -1032,7 +1036,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             if (qn > 1) pf1 = loadPrim(S, qref[1] & kPrimMask);
 #endif
 #pragma unroll
-            for (int k_ = 0; k_ < kLeafQ; k_++) {
+            for (int k_ = 0; k_ < LQ; k_++) {
                 const bool act = qn > 0;
                 if (__ballot(act) == 0) break;
                 tested = false;
@@ -1041,7 +1045,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 const uint32_t ref = qref[0];
                 const float lo = lq[0];
 #pragma unroll
-                for (int i = 0; i + 1 < kLeafQ; i++) { qref[i] = qref[i + 1]; lq[i] = lq[i + 1]; }
+                for (int i = 0; i + 1 < LQ; i++) { qref[i] = qref[i + 1]; lq[i] = lq[i + 1]; }
                 qn--;
                 const uint32_t k = ref & kPrimMask;
                 sph = (ref & kSphereBit) != 0;
