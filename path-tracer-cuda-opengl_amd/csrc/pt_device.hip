@@ -639,7 +639,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
 #endif
 constexpr int kLeafQ = PT_LEAF_QUEUE;
 #ifndef PT_LEAF_QUEUE_SAMPLE
-#define PT_LEAF_QUEUE_SAMPLE 2   // sample mode, binary tree: 1067 vs 1088 ms (depth 4); compat prefers 4 (1774 vs 1959)
+#define PT_LEAF_QUEUE_SAMPLE 2   // sample mode, binary tree, STACK <= 32; compat prefers 4 (C3 1774 vs 1959 ms)
 #endif
 #ifndef PT_WIDE_EXACT
 #define PT_WIDE_EXACT 0   // debug: re-test every wide-tree leaf from its vertices
@@ -792,7 +792,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
     float closest = 0.0f;
     int best = -1, depthLeft = 0, sample = 0, node = -1, sp = 0, qn = 0;
-    constexpr int LQ = (SAMPLE && !WIDE) ? PT_LEAF_QUEUE_SAMPLE : kLeafQ;   // leaf queue depth
+    // leaf queue depth: sample mode on shallow trees (STACK <= 32: C2, C3) prefers 2, deep trees
+    // (C5, STACK 48+) and compat mode 4 (C3 1068 vs 1088 ms, C2 67.4 vs 70.6, C5 1576 vs 1471)
+    constexpr int LQ = (SAMPLE && !WIDE && STACK <= 32) ? PT_LEAF_QUEUE_SAMPLE : kLeafQ;
     uint32_t qref[LQ];   // leaf queue: leaf refs in DFS order (registers: constant indices only)
     float lq[LQ];     // their slab entry distances
 #pragma unroll
