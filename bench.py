@@ -43,7 +43,9 @@ CONFIGS = {
     "c3": ("bunny_cornell", "bunny-in-Cornell (5,000 tris) 1920x1080 @1024spp depth 50 (C3)"),
     "c2": ("cornell", "Cornell box (32 tris) 800x800 @256spp depth 8 (C2)"),
     "c5": ("bunny_field", "1,043,312-tri bunny field 1920x1080 @512spp depth 16 (C5)"),
+    "c4": ("bunny_cornell", "bunny-in-Cornell (5,000 tris) 1920x1080 @4096spp depth 50 (C4, the 8-GPU config)"),
 }
+CONFIG_SPP = {"c4": 4096}
 STRIPE = 8
 
 
@@ -122,7 +124,7 @@ def main() -> None:
 
     name, workload = CONFIGS[args.config]
     preset = ptamd.Preset(name)
-    spp = args.spp or preset.spp
+    spp = args.spp or CONFIG_SPP.get(args.config, preset.spp)
     w, h, depth = preset.width, preset.height, preset.max_depth
     scene = ptamd.Scene(preset.objects, preset.materials, device=local)
     film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
