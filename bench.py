@@ -117,10 +117,18 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # nccl = RCCL over xGMI.  PT_DIST_BACKEND=gloo only rehearses the multi-rank flow (e.g. two
+    # ranks sharing one GPU, frames gathered through host memory); it never produces a reported number.
+    backend = os.environ.get("PT_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     name, workload = CONFIGS[args.config]
     preset = ptamd.Preset(name)
@@ -148,7 +156,12 @@ def main() -> None:
                              shade_batch=args.shade_batch, rng=ptamd.RNG_SAMPLE if sample else ptamd.RNG_COMPAT,
                              chunk=args.chunk, out_format=out_format)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, local_buf)
+            if backend == "nccl":
+                dist.all_gather_into_tensor(gathered, local_buf)
+            else:
+                parts = [torch.empty_like(local_buf, device="cpu") for _ in range(world)]
+                dist.all_gather(parts, local_buf.cpu())
+                gathered.copy_(torch.cat(parts))
         return st
 
     # Warmup 1 uses the ray-synchronous kernel, whose traversal follows the reference's node
@@ -178,7 +191,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         mx = t[:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
