@@ -176,3 +176,25 @@ def test_render_png_app(pt, orc, gpu, tmp_path, frames, rng):
         rgb, _ = pt.render(scene, film, p.camera, spp, 50, rng=pt.RNG_COMPAT if rng == "compat" else pt.RNG_SAMPLE,
                            accumulate=frames > 1)
     np.testing.assert_array_equal(read_png(out), pt.quantize_rgba8(rgb, w, h))
+
+
+def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
+    """bench.py's multi-rank flow (stripe partition, per-rank RGBA8 frames, gather, un-permute,
+    PNG) rehearsed with two ranks sharing the GPU over gloo: the PNG equals the 1-rank PNG."""
+    import os
+    import subprocess
+    import sys
+    from helpers import read_png
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--config", "c2", "--spp", "4", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+              "--no-compat"]
+    one, two = str(tmp_path / "one.png"), str(tmp_path / "two.png")
+    r1 = subprocess.run([sys.executable] + common + ["--png", one], cwd=repo, capture_output=True, text=True,
+                        timeout=300)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    env = dict(os.environ, PT_DIST_BACKEND="gloo")
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                         "--master-addr", "127.0.0.1", "--master-port", "29517"] + common[:1] + ["--gpus", "2"] +
+                        common[1:] + ["--png", two], cwd=repo, capture_output=True, text=True, timeout=300, env=env)
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    np.testing.assert_array_equal(read_png(one), read_png(two))
