@@ -252,6 +252,29 @@ def test_full_size_c5_bvh_and_trace(pt, orc, gpu):
     assert_hits_equal(hits, rh)
 
 
+@pytest.mark.parametrize("kernel", ["wavefront", "wide"])
+def test_c5_deep_tree_render_bit_exact(pt, orc, gpu, kernel):
+    """C5's 1,043,312-triangle LBVH is deep (large LDS stack, leaf queue 4 in sample mode): a small
+    frame of the C5 scene in both RNG modes, bit-exact against the oracle."""
+    w, h, depth = 48, 27, 16
+    p = pt.Preset("bunny_field", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    assert s.bvh_info()["depth"] >= 32   # depth + 1 > 32: the STACK = 48 instantiations
+    k = pt.KERNEL_WAVEFRONT if kernel == "wavefront" else pt.KERNEL_WIDE
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    cam = pt.camera_to_array(p.camera)
+    f = pt.Film(w, h, 3, device=gpu)
+    rgb, st = pt.render(s, f, p.camera, 2, depth, kernel=k)
+    ref, rst = orc.render(p.objects, p.materials, nodes, cam, w, h, f.rows, 2, depth, orc.film_states(3, w, f.rows),
+                          nthreads=8)
+    np.testing.assert_array_equal(bits(rgb), bits(ref))
+    assert st.tri_tests == rst.tri_tests
+    srgb, sst = pt.render(s, f, p.camera, 5, depth, rng=pt.RNG_SAMPLE, chunk=2, kernel=k)
+    sref, srst = orc.render_sample(p.objects, p.materials, nodes, cam, w, h, f.rows, 5, depth, 3, 2, nthreads=8)
+    np.testing.assert_array_equal(bits(srgb), bits(sref))
+    assert sst.tri_tests == srst.tri_tests
+
+
 def test_device_output_pointer(gpu):
     """pt_render into a caller-owned device buffer (a torch tensor) on the caller's stream.
     Runs in a child process that imports torch BEFORE libpt.so, as bench.py does, so that both
