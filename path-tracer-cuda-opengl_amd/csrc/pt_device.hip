@@ -50,7 +50,8 @@ constexpr int kWave = 64;
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kPrimMask = 0x3fffffffu;
-constexpr int kJumpMats = 32;                    // XORWOW 2^(67+k) jump matrices, k < 32
+constexpr int kJumpMats = 32;
+constexpr int kNumCounters = 32;                 // per-scene u64 counters: work counts, error word, diagnostics                    // XORWOW 2^(67+k) jump matrices, k < 32
 
 // ------------------------------------------------------------------------ device structs
 struct DevScene {
@@ -778,6 +779,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
 #ifdef PT_DIAG
     uint32_t itN = 0, itL = 0, itS = 0, sPops = 0;   // scheduler diagnostics (iterations per kind)
     unsigned long long cycN = 0, cycL = 0, cycS = 0;   // and shader cycles per kind
+    unsigned long long cycSh = 0, cycTk = 0, cycNp = 0, cycBr = 0;   // SHADE: shading, tasks, new path, ray start
 #define PT_DIAG_ADD(v, x) (v) += (x)
 #else
 #define PT_DIAG_ADD(v, x) ((void)0)
@@ -1105,6 +1107,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 newRay = true;   // bounce, next sample (newSample) or finished (reset below)
                 if (!active) newRay = false;
             }
+#ifdef PT_DIAG
+            const unsigned long long tS1 = __builtin_amdgcn_s_memtime();
+#endif
             if constexpr (SAMPLE) {   // idle lanes take new tasks and start their first path
                 bool got = false;
                 PT_TAKE_TASKS(got);
@@ -1114,8 +1119,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 }
             }
             // one camera-ray and one ray-start site for every lane that needs them
+#ifdef PT_DIAG
+            const unsigned long long tS2 = __builtin_amdgcn_s_memtime();
+#endif
             if (newSample) PT_NEW_PATH();
+#ifdef PT_DIAG
+            const unsigned long long tS3 = __builtin_amdgcn_s_memtime();
+#endif
             if (newRay) PT_BEGIN_RAY();
+#ifdef PT_DIAG
+            const unsigned long long tS4 = __builtin_amdgcn_s_memtime();
+            cycSh += tS1 - tK0; cycTk += tS2 - tS1; cycNp += tS3 - tS2; cycBr += tS4 - tS3;
+#endif
             sRays += (uint32_t)__popcll(__ballot(newRay));
             sPaths += (uint32_t)__popcll(__ballot(newSample));
         }
@@ -1160,6 +1175,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
         atomicAdd(P.counters + 12, cycN);
         atomicAdd(P.counters + 13, cycL);
         atomicAdd(P.counters + 14, cycS);
+        atomicAdd(P.counters + 16, cycSh);
+        atomicAdd(P.counters + 17, cycTk);
+        atomicAdd(P.counters + 18, cycNp);
+        atomicAdd(P.counters + 19, cycBr);
 #endif
     }
 }
@@ -1865,7 +1884,7 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
     }
     if ((rc = devAlloc(s->mats, m.size() * sizeof(float4)))) return rc;
     HIP_TRY(hipMemcpy(s->mats.p, m.data(), m.size() * sizeof(float4), hipMemcpyHostToDevice));
-    if ((rc = devAlloc(s->counters, 16 * sizeof(unsigned long long)))) return rc;
+    if ((rc = devAlloc(s->counters, kNumCounters * sizeof(unsigned long long)))) return rc;
     if ((rc = devAlloc(s->dobjs, (size_t)std::max<int64_t>(1, n) * sizeof(pt_object)))) return rc;
     if (n > 0) HIP_TRY(hipMemcpy(s->dobjs.p, objs, (size_t)n * sizeof(pt_object), hipMemcpyHostToDevice));
     *out = s.release();
@@ -2049,7 +2068,7 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     DevBuf dr, dh;
     if ((rc = devAlloc(dr, n * sizeof(pt_ray))) || (rc = devAlloc(dh, n * sizeof(pt_hit)))) return rc;
     if (n > 0) HIP_TRY(hipMemcpy(dr.p, rays, n * sizeof(pt_ray), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(s->counters.p, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->counters.p, 0, kNumCounters * sizeof(unsigned long long)));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -2066,7 +2085,7 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (n > 0) HIP_TRY(hipMemcpy(hits, dh.p, n * sizeof(pt_hit), hipMemcpyDeviceToHost));
-    unsigned long long c[16] = {0};
+    unsigned long long c[kNumCounters] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     c[4] = 0;
     fillStats(stats, c, ms);
@@ -2194,7 +2213,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = devAlloc(dout, (size_t)std::max<int64_t>(1, np) * outBpp))) return rc;
         dst = dout.p;
     }
-    HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16 * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(s->counters.p, 0, kNumCounters * sizeof(unsigned long long), st));
     RenderParams P;
     P.S = devScene(s);
     P.cam.pos = make_float3(cam->origin[0], cam->origin[1], cam->origin[2]);
@@ -2366,7 +2385,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         }
     }
     if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * outBpp, hipMemcpyDeviceToHost));
-    unsigned long long c[16] = {0};
+    unsigned long long c[kNumCounters] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     fillStats(stats, c, ms);
     if (std::getenv("PT_ITER_STATS") && c[8] + c[9] + c[10] > 0)   // diagnostic: wavefront scheduler
@@ -2378,6 +2397,10 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                      "shade %.3f\n", (double)c[12] / std::max(1ull, c[8]), (double)c[13] / std::max(1ull, c[9]),
                      (double)c[14] / std::max(1ull, c[10]), (double)c[12] / (double)(c[12] + c[13] + c[14]),
                      (double)c[13] / (double)(c[12] + c[13] + c[14]), (double)c[14] / (double)(c[12] + c[13] + c[14]));
+    if (std::getenv("PT_ITER_STATS") && c[14] > 0)
+        std::fprintf(stderr, "[pt] SHADE cycles/iteration: shading %.0f tasks %.0f new-path %.0f ray-start %.0f\n",
+                     (double)c[16] / std::max(1ull, c[10]), (double)c[17] / std::max(1ull, c[10]),
+                     (double)c[18] / std::max(1ull, c[10]), (double)c[19] / std::max(1ull, c[10]));
     if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
     return PT_OK;
 }
