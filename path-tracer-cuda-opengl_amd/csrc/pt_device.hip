@@ -651,7 +651,7 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #ifndef PT_TASK_POOL
 #define PT_TASK_POOL 64
 #endif
-constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic (64 near the end)
+constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
 #ifndef PT_WAVES_PER_EU
 #define PT_WAVES_PER_EU 4
 #endif
@@ -844,9 +844,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             if (poolLeft == 0u) { /* refill the wave's pool: one returning atomic per kTaskPool */ \
                 const int leader_ = __ffsll((unsigned long long)m_) - 1;                          \
                 uint32_t b_ = 0;                                                                  \
-                /* large grabs while far from the end, small ones for the tail */                 \
-                const uint32_t grab_ = poolBase + 8u * (uint32_t)kTaskPool * (uint32_t)P.nwaves < P.ntasks \
-                                           ? (uint32_t)kTaskPool : 64u;                           \
+                /* always a full pool: = one (tile, block) group, one task per lane; smaller    \
+                   grabs near the end measured slower (1/8 share: 150-158 vs 145 ms) */          \
+                const uint32_t grab_ = (uint32_t)kTaskPool;                                       \
                 if (lane == leader_) b_ = atomicAdd(P.taskCounter, grab_);                        \
                 poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
                 poolLeft = grab_;                                                                 \
