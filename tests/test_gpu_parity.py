@@ -190,6 +190,21 @@ def test_render_edge_cases(pt, orc, gpu, kernel):
     one.objects, one.materials = objs, mats
     rgb, _, _, ref, _, _, _ = render_both(pt, orc, gpu, one, 16, 9, 2, 5)
     np.testing.assert_array_equal(bits(rgb), bits(ref))
+    # no objects at all (every path is the sky), and a 1x1 frame, in both RNG modes
+    empty = pt.Preset("rtiow", 16, 9)
+    empty.objects = empty.objects[:0]
+    rgb, st, _, ref, _, _, _ = render_both(pt, orc, gpu, empty, 16, 9, 3, 50)
+    np.testing.assert_array_equal(bits(rgb), bits(ref))
+    assert st.rays == 16 * 9 * 3 and st.node_visits == 0
+    for scene in (empty, pt.Preset("rtiow", 1, 1)):
+        w, h = (16, 9) if scene is empty else (1, 1)
+        s = pt.Scene(scene.objects, scene.materials, device=gpu)
+        srgb, _ = pt.render(s, pt.Film(w, h, 4, device=gpu), scene.camera, 5, 50, rng=pt.RNG_SAMPLE, chunk=2)
+        nodes = orc.build_lbvh(scene.objects, orc.morton_keys(scene.objects), tight=True) if len(scene.objects) \
+            else np.zeros(0, pt.NODE_DTYPE)
+        sref, _ = orc.render_sample(scene.objects, scene.materials, nodes, pt.camera_to_array(scene.camera), w, h,
+                                    np.arange(h, dtype=np.int32), 5, 50, 4, 2, nthreads=2)
+        np.testing.assert_array_equal(bits(srgb), bits(sref))
 
 
 def test_render_continues_streams(pt, orc, gpu):
