@@ -992,6 +992,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 const SlabHit hr = slabRight(b, q, o, inv, 0.001f, closest);
 #endif
                 // append hit leaves in order (left, then right) with their slab entry distances
+                if constexpr (LQ == 2) {
+                    // a NODE step needs an empty queue (qn <= LQ - 2): the slots are fixed
+                    const bool al = hl.hit && (lref & kLeafBit), ar = hr.hit && (rref & kLeafBit);
+                    qref[0] = al ? lref : rref;
+                    lq[0] = al ? hl.lo : hr.lo;
+                    qref[1] = rref;
+                    lq[1] = hr.lo;
+                    qn = (al ? 1 : 0) + (ar ? 1 : 0);
+                } else {
                 if (hl.hit && (lref & kLeafBit)) {
 #pragma unroll
                     for (int i = 0; i < LQ; i++) {
@@ -1007,6 +1016,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                         lq[i] = qn == i ? hr.lo : lq[i];
                     }
                     qn++;
+                }
                 }
                 const bool il = hl.hit && !(lref & kLeafBit), ir = hr.hit && !(rref & kLeafBit);
                 // push left then right, pop: descend straight into the child that would be popped
