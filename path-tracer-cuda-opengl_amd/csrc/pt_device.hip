@@ -1019,12 +1019,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 }
                 }
                 const bool il = hl.hit && !(lref & kLeafBit), ir = hr.hit && !(rref & kLeafBit);
-                // push left then right, pop: descend straight into the child that would be popped
+                // push left then right, pop: descend straight into the child that would be popped.
+                // No overflow check: an entry is pushed only for a left sibling on the current
+                // path, one per level, so sp < depth <= STACK - 1 (stackFor).
                 if (ir) {
-                    if (il) {
-                        if (sp < STACK) { my[sp * kWave] = lref; sp++; }
-                        else { atomicOr(S.err, 2u); }
-                    }
+                    if (il) { my[sp * kWave] = lref; sp++; }
                     node = (int)rref;
                 } else if (il) {
                     node = (int)lref;
