@@ -648,6 +648,9 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #ifndef PT_LEAF_PREFETCH
 #define PT_LEAF_PREFETCH 1
 #endif
+#ifndef PT_NODE_BUFFER_LOADS
+#define PT_NODE_BUFFER_LOADS 1
+#endif
 #ifndef PT_TASK_POOL
 #define PT_TASK_POOL 64
 #endif
@@ -772,6 +775,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     float fcol = (float)col;
     float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
+#if PT_NODE_BUFFER_LOADS
+    // gfx9 buffer resource: base = the node array, raw (stride 0), DATA_FORMAT_32 in dword 3
+    const __amdgpu_buffer_rsrc_t nodeRsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)S.nodes, 0, 0x7fffffff, 0x00020000);
+#endif
     uint32_t* my = stk + lane;
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
@@ -978,8 +986,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             if constexpr (WIDE) {
                 if (wantNode) wideNodeStep<STACK>(S, node, sp, qn, qref, lq, my, o, inv, closest);
             } else if (wantNode) {
+#if PT_NODE_BUFFER_LOADS
+                // buffer loads: a 32-bit per-lane offset off a wave-uniform resource (no 64-bit
+                // address arithmetic per visit); < 2^26 nodes (pt_scene_create)
+                const uint32_t off = (uint32_t)node * 64u;
+                const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+                const float4 b = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+                const float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+                const float4 r = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+#else
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
+#endif
                 const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
 #if PT_PACKED_SLAB
                 SlabHit2 h2 = slabBoth(a, b, q, o, inv, 0.001f, closest);
@@ -1869,7 +1887,7 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
                     pt_scene** out) {
     if (!out || n < 0 || nmat < 0 || (n > 0 && !objs) || (nmat > 0 && !mats))
         return fail(PT_ERR_INVALID, "pt_scene_create: bad argument");
-    if (n >= (int64_t)kPrimMask) return fail(PT_ERR_INVALID, "pt_scene_create: too many objects");
+    if (n >= ((int64_t)1 << 26)) return fail(PT_ERR_INVALID, "pt_scene_create: more than 2^26 objects");
     for (int64_t i = 0; i < n; i++) {
         if (objs[i].type != PT_SPHERE && objs[i].type != PT_TRIANGLE)
             return fail(PT_ERR_INVALID, "pt_scene_create: unknown object type");
