@@ -47,6 +47,9 @@ hipError_t radixSortPairs(void* temp, size_t* temp_bytes, const uint32_t* codes_
 namespace {
 
 constexpr int kWave = 64;
+#ifndef PT_BUFFER_LOADS
+#define PT_BUFFER_LOADS 0   // primitive/shading records through buffer loads: measured 999 vs 995 ms (off)
+#endif
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kPrimMask = 0x3fffffffu;
@@ -223,9 +226,25 @@ __device__ __forceinline__ SlabHit slabRight(float4 b, float4 q, float3 o, float
 // Primitive record (leaf order), 3 x float4:
 //   triangle {v0, mat} {v1, objID} {v2, 0}        sphere {c, mat} {r, 0, 0, objID} {0, 0, 0, 1}
 struct Prim { float4 p0, p1, p2; };
+// Raw gfx9 buffer resource over a device array (stride 0, DATA_FORMAT_32): per-lane loads then
+// take a 32-bit offset instead of 64-bit address arithmetic.  Arrays stay below 4 GB (< 2^26
+// primitives / nodes, pt_scene_create).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rawRsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1 /* 4 GB of records */, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 __device__ __forceinline__ Prim loadPrim(const DevScene& S, uint32_t k) {
+#if PT_BUFFER_LOADS
+    const __amdgpu_buffer_rsrc_t r = rawRsrc(S.prims);
+    const uint32_t off = k * 48u;
+    return Prim{bload4(r, off), bload4(r, off + 16u), bload4(r, off + 32u)};
+#else
     const float4* p = S.prims + 3 * (size_t)k;
     return Prim{p[0], p[1], p[2]};
+#endif
 }
 
 // Exact object box (cuda_object.h:21-42: sphere c -/+ |r|; triangle via utils::unionPoints)
@@ -347,8 +366,14 @@ struct HitRec { float3 p, n; int mat, obj; bool front; float4 m0; float ir; int 
 
 __device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, float3 o, float3 d) {
     HitRec h;
+#if PT_BUFFER_LOADS
+    const __amdgpu_buffer_rsrc_t rs = rawRsrc(S.shade);
+    const uint32_t off = (uint32_t)k * 48u;
+    const float4 s0 = bload4(rs, off), s1 = bload4(rs, off + 16u), s2 = bload4(rs, off + 32u);
+#else
     const float4* r = S.shade + 3 * (size_t)k;
     const float4 s0 = r[0], s1 = r[1], s2 = r[2];
+#endif
     const uint32_t tf = __float_as_uint(s2.y);
     h.p = add(o, scale(t, d));
     float3 outward;
@@ -777,8 +802,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
     const DevScene& S = P.S;
 #if PT_NODE_BUFFER_LOADS
     // gfx9 buffer resource: base = the node array, raw (stride 0), DATA_FORMAT_32 in dword 3
-    const __amdgpu_buffer_rsrc_t nodeRsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)S.nodes, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(S.nodes);
 #endif
     uint32_t* my = stk + lane;
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
@@ -990,10 +1014,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                 // buffer loads: a 32-bit per-lane offset off a wave-uniform resource (no 64-bit
                 // address arithmetic per visit); < 2^26 nodes (pt_scene_create)
                 const uint32_t off = (uint32_t)node * 64u;
-                const float4 a = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
-                const float4 b = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
-                const float4 q = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
-                const float4 r = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+                const float4 a = bload4(nodeRsrc, off), b = bload4(nodeRsrc, off + 16u);
+                const float4 q = bload4(nodeRsrc, off + 32u), r = bload4(nodeRsrc, off + 48u);
 #else
                 const float4* np = S.nodes + 4 * (size_t)node;
                 const float4 a = np[0], b = np[1], q = np[2], r = np[3];
