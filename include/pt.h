@@ -128,6 +128,12 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n_objects,
 #define PT_BVH_ORIGIN_BOUNDS 1
 #define PT_BVH_HOST_KEYS 2
 int pt_scene_build_bvh(pt_scene* scene, int flags);
+/* Dynamic scenes (per-frame rebuild): overwrite objects [first, first + n)
+ * (host array; same validation as pt_scene_create) and mark the hierarchy stale -- rendering or
+ * tracing fails with PT_ERR_STATE until pt_scene_build_bvh runs again.  A rebuild reuses every
+ * device buffer of the previous build (no allocation, no device-wide synchronisation).  The
+ * reference has no counterpart: it builds once (main.cu:122-128 / bvh.h:132-145). */
+int pt_scene_update_objects(pt_scene* scene, const pt_object* objs, int64_t first, int64_t n);
 /* Device time of the last pt_scene_build_bvh (HIP events around the build's stream work). */
 int pt_scene_build_time(pt_scene* scene, double* ms);
 int pt_scene_bvh_info(pt_scene* scene, int* depth, int64_t* n_nodes, int64_t* device_bytes);

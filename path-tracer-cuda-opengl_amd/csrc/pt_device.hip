@@ -1642,19 +1642,27 @@ const std::vector<uint32_t>& jumpMatrices() {
 
 struct DevBuf {
     void* p = nullptr;
+    size_t cap = 0;   // bytes allocated
     ~DevBuf() { if (p) (void)hipFree(p); }
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     template <class T> T* as() const { return static_cast<T*>(p); }
-    void reset() { if (p) (void)hipFree(p); p = nullptr; }
+    void reset() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
 };
 
 int devAlloc(DevBuf& b, size_t bytes) {
-    if (b.p) { (void)hipFree(b.p); b.p = nullptr; }
+    b.reset();
     if (bytes == 0) bytes = 16;
     HIP_TRY(hipMalloc(&b.p, bytes));
+    b.cap = bytes;
     return PT_OK;
+}
+// Keeps the buffer when it is large enough (no hipFree / hipMalloc, which synchronise the device:
+// a per-frame BVH rebuild reuses every buffer of the previous build).
+int devReserve(DevBuf& b, size_t bytes) {
+    if (b.p && b.cap >= std::max<size_t>(bytes, 16)) return PT_OK;
+    return devAlloc(b, bytes);
 }
 
 int envInt(const char* name, int dflt) {
@@ -1686,6 +1694,9 @@ struct pt_scene {
     DevBuf dobjs;                           // the objects on the device (BVH build input)
     DevBuf mats, nodes, prims, shade, counters;
     DevBuf keys, iparent, lparent, leafBoxes;   // sorted 64-bit Morton keys, parent links, leaf boxes
+    // build scratch, kept between builds: codes / ids (unsorted, sorted), scene box, sphere
+    // flags, refit arrival counters, depth, sort temporary
+    DevBuf codes, ids, codes2, ids2, box6, sph, arr, dep, sortTemp;
     DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelWF<.., WIDE>), built on first use
     int wideDepth = 0;
     int64_t wideNodes = 0;
@@ -1940,6 +1951,24 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
     return PT_OK;
 }
 
+int pt_scene_update_objects(pt_scene* s, const pt_object* objs, int64_t first, int64_t n) {
+    if (!s || first < 0 || n < 0 || first > s->nobj || n > s->nobj - first || (n > 0 && !objs))
+        return fail(PT_ERR_INVALID, "pt_scene_update_objects: bad argument");
+    for (int64_t i = 0; i < n; i++) {
+        if (objs[i].type != PT_SPHERE && objs[i].type != PT_TRIANGLE)
+            return fail(PT_ERR_INVALID, "pt_scene_update_objects: unknown object type");
+        if (objs[i].mat < 0 || objs[i].mat >= s->nmat)
+            return fail(PT_ERR_INVALID, "pt_scene_update_objects: material id out of range");
+    }
+    int rc = setDevice(s->device);
+    if (rc) return rc;
+    if (n == 0) return PT_OK;
+    std::copy(objs, objs + n, s->objs.begin() + first);
+    HIP_TRY(hipMemcpy(s->dobjs.as<pt_object>() + first, objs, (size_t)n * sizeof(pt_object), hipMemcpyHostToDevice));
+    s->built = false;   // the hierarchy no longer matches the objects: rebuild before rendering
+    return PT_OK;
+}
+
 int pt_scene_build_bvh(pt_scene* s, int flags) {
     if (!s) return fail(PT_ERR_INVALID, "pt_scene_build_bvh: null scene");
     int rc = setDevice(s->device);
@@ -1953,15 +1982,16 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     // leaf records -> Karras hierarchy -> refit -> depth.  (PT_BVH_HOST_KEYS: the keys come from
     // the host restatement of computeMortonOnHost instead; the result is identical.)
     const size_t n1 = (size_t)std::max<int64_t>(1, n), ni = (size_t)std::max<int64_t>(1, n - 1);
-    if ((rc = devAlloc(s->prims, n1 * 3 * sizeof(float4))) || (rc = devAlloc(s->shade, n1 * 3 * sizeof(float4))) ||
-        (rc = devAlloc(s->nodes, ni * 4 * sizeof(float4))) || (rc = devAlloc(s->keys, n1 * 8)) ||
-        (rc = devAlloc(s->leafBoxes, n1 * 24)) || (rc = devAlloc(s->iparent, ni * 4)) ||
-        (rc = devAlloc(s->lparent, n1 * 4)))
+    if ((rc = devReserve(s->prims, n1 * 3 * sizeof(float4))) || (rc = devReserve(s->shade, n1 * 3 * sizeof(float4))) ||
+        (rc = devReserve(s->nodes, ni * 4 * sizeof(float4))) || (rc = devReserve(s->keys, n1 * 8)) ||
+        (rc = devReserve(s->leafBoxes, n1 * 24)) || (rc = devReserve(s->iparent, ni * 4)) ||
+        (rc = devReserve(s->lparent, n1 * 4)))
         return rc;
-    DevBuf codes, ids, codes2, ids2, box6, sph, arr, dep, temp;
-    if ((rc = devAlloc(codes, n1 * 4)) || (rc = devAlloc(ids, n1 * 4)) || (rc = devAlloc(codes2, n1 * 4)) ||
-        (rc = devAlloc(ids2, n1 * 4)) || (rc = devAlloc(box6, 64)) || (rc = devAlloc(sph, n1 * 4)) ||
-        (rc = devAlloc(arr, ni * 4)) || (rc = devAlloc(dep, 16)))
+    DevBuf &codes = s->codes, &ids = s->ids, &codes2 = s->codes2, &ids2 = s->ids2, &box6 = s->box6, &sph = s->sph,
+           &arr = s->arr, &dep = s->dep, &temp = s->sortTemp;
+    if ((rc = devReserve(codes, n1 * 4)) || (rc = devReserve(ids, n1 * 4)) || (rc = devReserve(codes2, n1 * 4)) ||
+        (rc = devReserve(ids2, n1 * 4)) || (rc = devReserve(box6, 64)) || (rc = devReserve(sph, n1 * 4)) ||
+        (rc = devReserve(arr, ni * 4)) || (rc = devReserve(dep, 16)))
         return rc;
     hipStream_t st = 0;
     hipEvent_t e0, e1;
@@ -1987,7 +2017,7 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
             size_t tbytes = 0;
             HIP_TRY(pt::radixSortPairs(nullptr, &tbytes, codes.as<uint32_t>(), codes2.as<uint32_t>(),
                                        ids.as<uint32_t>(), ids2.as<uint32_t>(), (size_t)n, 30, st));
-            if ((rc = devAlloc(temp, tbytes))) return rc;
+            if ((rc = devReserve(temp, tbytes))) return rc;
             HIP_TRY(pt::radixSortPairs(temp.p, &tbytes, codes.as<uint32_t>(), codes2.as<uint32_t>(),
                                        ids.as<uint32_t>(), ids2.as<uint32_t>(), (size_t)n, 30, st));
         }

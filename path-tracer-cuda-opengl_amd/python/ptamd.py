@@ -77,6 +77,7 @@ EXPORTS = [
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
     "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
+    "pt_scene_update_objects",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -101,6 +102,7 @@ _sig = {
     "pt_scene_create": (C.c_int, [C.c_int, _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_void_p)]),
     "pt_scene_build_bvh": (C.c_int, [_P, C.c_int]),
     "pt_scene_build_time": (C.c_int, [_P, C.POINTER(C.c_double)]),
+    "pt_scene_update_objects": (C.c_int, [_P, _P, C.c_int64, C.c_int64]),
     "pt_scene_bvh_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "pt_scene_download_bvh": (C.c_int, [_P, _P]),
     "pt_trace_closest": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, _P, C.POINTER(Stats)]),
@@ -241,6 +243,15 @@ class Scene:
 
     def build_bvh(self, flags: int = PT_BVH_ORIGIN_BOUNDS) -> None:
         _check(lib.pt_scene_build_bvh(self.h, flags), "pt_scene_build_bvh")
+
+    def update_objects(self, objects: np.ndarray, first: int = 0) -> None:
+        """Overwrite objects [first, first + len(objects)); the BVH must be rebuilt (build_bvh)
+        before the next render or trace (dynamic scenes, one rebuild per frame)."""
+        objs = np.ascontiguousarray(objects, OBJECT_DTYPE)
+        _check(lib.pt_scene_update_objects(self.h, _ptr(objs) if len(objs) else None, first, len(objs)),
+               "pt_scene_update_objects")
+        self.objects = self.objects.copy()
+        self.objects[first:first + len(objs)] = objs
 
     @property
     def build_ms(self) -> float:
