@@ -680,9 +680,15 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #define PT_TASK_POOL 64
 #endif
 constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
+// Occupancy target of the wavefront kernel: 5 waves per SIMD = at most 96 VGPRs (C3 sample
+// mode 910 -> 873 ms vs 4 waves; LDS caps deep trees, STACK 48+, at 4 or fewer)
 #ifndef PT_WAVES_PER_EU
-#define PT_WAVES_PER_EU 4
+#define PT_WAVES_PER_EU 5
 #endif
+// per stack depth: the LDS stack (STACK x 256 B per wave) allows 4 / 3 / 2 waves per SIMD at
+// STACK 48 / 64 / 80 (160 KB per CU), so those keep the larger register budget
+template <int STACK>
+constexpr int kWavesPerEU = STACK <= 32 ? PT_WAVES_PER_EU : (STACK <= 48 ? 4 : (STACK <= 64 ? 3 : 2));
 
 // One NODE step on the 4-wide tree for one lane.  Entries of a wide node are in the reference's
 // DFS order: leading hit leaves go to the leaf queue (with their entry distance), the first hit
@@ -779,7 +785,7 @@ __device__ __forceinline__ void wideNodeStep(const DevScene& S, int& node, int& 
 // slab entry distance; leaves that wait on the stack behind an internal entry are queued with
 // lo = -inf and re-tested exactly from the primitive's vertices (primBoxHit).
 template <int STACK, bool SAMPLE, bool WIDE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_PER_EU))) void renderKernelWF(RenderParams P) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK>))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
@@ -1074,7 +1080,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
                     node = -1;
                 }
             }
-        } else if (kind == 1) {
+        }
+        if (kind == 1) {
             // ------------------------------------------------------------------ LEAF
             bool tested = false, sph = false;
             PT_DIAG_ADD(itL, 1u);
@@ -1122,7 +1129,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_WAVES_
             sTris += (uint32_t)__popcll(__ballot(tested && !sph));
             sSph += (uint32_t)__popcll(__ballot(tested && sph));
             }
-        } else {
+        }
+        if (kind == 2) {
             // ------------------------------------------------------------------ SHADE
             bool newRay = false, newSample = false;
             PT_DIAG_ADD(itS, 1u);
@@ -1834,6 +1842,26 @@ void launchRender(const RenderParams& P, hipStream_t st) {
     else if (P.partial) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
+template <int S>
+int wavesPerCU(int kernel, int& n) {
+    const void* fn = kernel == PT_KERNEL_WIDE ? reinterpret_cast<const void*>(&renderKernelWF<S, true, true>)
+                                              : reinterpret_cast<const void*>(&renderKernelWF<S, true, false>);
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kWave, 0));
+    return PT_OK;
+}
+int persistentWavesPerCU(int stack, int kernel, int& n) {
+    switch (stack) {
+        case 16: return wavesPerCU<16>(kernel, n);
+#ifdef PT_STACK24
+        case 24: return wavesPerCU<24>(kernel, n);
+#endif
+        case 32: return wavesPerCU<32>(kernel, n);
+        case 48: return wavesPerCU<48>(kernel, n);
+        case 64: return wavesPerCU<64>(kernel, n);
+        case 80: return wavesPerCU<80>(kernel, n);
+        default: return fail(PT_ERR_STATE, "unsupported BVH depth");
+    }
+}
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
     switch (stack) {
         case 16: launchRender<16>(P, st); break;
@@ -2386,8 +2414,11 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                 f->cus = 256;
             f->cus = std::max(f->cus, 1);
         }
-        // persistent: enough waves to fill every SIMD (4 per CU, PT_WAVES_PER_EU each)
-        const uint64_t full = (uint64_t)f->cus * 4 * PT_WAVES_PER_EU;
+        // persistent: exactly the waves that fit at once (the kernel's occupancy per CU, which
+        // the LDS stack caps below PT_WAVES_PER_EU per SIMD on deep trees)
+        int perCU = 0;
+        if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
+        const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
     }
