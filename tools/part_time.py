@@ -20,13 +20,15 @@ scene = ptamd.Scene(p.objects, p.materials)
 for part in sorted({0, n // 2, n - 1}):
     f = ptamd.Film(p.width, p.height, 1, stripe_height=8, n_parts=n, part=part)
     out = torch.empty((f.n_pixels * 3,), dtype=torch.float32, device="cuda")
-    times = []
+    times, kms = [], []
     for it in range(3):
         f.reset()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        _, st = ptamd.render(scene, f, p.camera, spp, p.max_depth, out=out.data_ptr(), rng=rng)
+        _, st = ptamd.render(scene, f, p.camera, spp, p.max_depth, out=out.data_ptr(), rng=rng,
+                             flags=ptamd.IDENTITY_ORDER if os.environ.get("IDENTITY") else 0)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
+        kms.append(st.kernel_ms)
     print(json.dumps({"n_parts": n, "part": part, "mode": mode, "ms": [round(t * 1e3, 1) for t in times],
-                      "rays": st.rays}), flush=True)
+                      "kernel_ms": [round(k, 1) for k in kms], "rays": st.rays}), flush=True)
