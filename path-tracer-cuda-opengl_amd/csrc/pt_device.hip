@@ -680,15 +680,24 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #define PT_TASK_POOL 64
 #endif
 constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
-// Occupancy target of the wavefront kernel: 5 waves per SIMD = at most 96 VGPRs (C3 sample
-// mode 910 -> 873 ms vs 4 waves; LDS caps deep trees, STACK 48+, at 4 or fewer)
+// Occupancy target of the wavefront kernel (waves per SIMD; 6 = at most 80 VGPRs).  The LDS
+// stack (STACK x 256 B per wave, 160 KB per CU) allows 6 / 5 / 4 / 3 / 2 waves per SIMD at
+// STACK 24 / 32 / 48 / 64 / 80, so deeper trees keep a larger register budget.  Compat tile
+// mode measured best at 5 (C3 1,617 vs 1,675 ms at 6).  Sample mode on C3 (STACK 24):
+// 4 waves 910 ms, 5 waves 815 ms, 6 waves 754 ms.
 #ifndef PT_WAVES_PER_EU
-#define PT_WAVES_PER_EU 5
+#define PT_WAVES_PER_EU 6
 #endif
-// per stack depth: the LDS stack (STACK x 256 B per wave) allows 4 / 3 / 2 waves per SIMD at
-// STACK 48 / 64 / 80 (160 KB per CU), so those keep the larger register budget
+#ifndef PT_STACK24
+#define PT_STACK24 1   // STACK 24 instantiations (C3: depth + 1 <= 24): 6 waves per SIMD fit the LDS
+#endif
+// Compat tile launches on shallow trees: dynamic LDS padding to 8 KB per wave caps them at
+// 5 waves per SIMD (their registers would allow 6, which measured slower: 1,670 vs 1,617 ms)
 template <int STACK>
-constexpr int kWavesPerEU = STACK <= 32 ? PT_WAVES_PER_EU : (STACK <= 48 ? 4 : (STACK <= 64 ? 3 : 2));
+constexpr unsigned kCompatPad = STACK * 256 < 8192 ? 8192u - STACK * 256u : 0u;
+template <int STACK, bool SAMPLE>
+constexpr int kWavesPerEU = STACK <= 24 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
+                                        : (STACK <= 32 ? 5 : (STACK <= 48 ? 4 : (STACK <= 64 ? 3 : 2)));
 
 // One NODE step on the 4-wide tree for one lane.  Entries of a wide node are in the reference's
 // DFS order: leading hit leaves go to the leaf queue (with their entry distance), the first hit
@@ -785,7 +794,7 @@ __device__ __forceinline__ void wideNodeStep(const DevScene& S, int& node, int& 
 // slab entry distance; leaves that wait on the stack behind an internal entry are queued with
 // lo = -inf and re-tested exactly from the primitive's vertices (primBoxHit).
 template <int STACK, bool SAMPLE, bool WIDE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK>))) void renderKernelWF(RenderParams P) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE>))) void renderKernelWF(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
@@ -1683,7 +1692,7 @@ int envInt(const char* name, int dflt) {
 
 int stackFor(int depth) {
     const int need = depth + 1;
-#ifdef PT_STACK24
+#if PT_STACK24
     for (int s : {16, 24, 32, 48, 64, 80})
 #else
     for (int s : {16, 32, 48, 64, 80})
@@ -1835,10 +1844,11 @@ int setDevice(int dev) {
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
     if (P.kernel == PT_KERNEL_WIDE && P.partial) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WIDE) renderKernelWF<S, false, true><<<P.ntiles, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WIDE) renderKernelWF<S, false, true><<<P.ntiles, kWave, kCompatPad<S>, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
         renderKernelWF<S, true, false><<<P.nwaves, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WAVEFRONT) renderKernelWF<S, false, false><<<P.ntiles, kWave, 0, st>>>(P);
+    else if (P.kernel == PT_KERNEL_WAVEFRONT)
+        renderKernelWF<S, false, false><<<P.ntiles, kWave, kCompatPad<S>, st>>>(P);
     else if (P.partial) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
@@ -1852,7 +1862,7 @@ int wavesPerCU(int kernel, int& n) {
 int persistentWavesPerCU(int stack, int kernel, int& n) {
     switch (stack) {
         case 16: return wavesPerCU<16>(kernel, n);
-#ifdef PT_STACK24
+#if PT_STACK24
         case 24: return wavesPerCU<24>(kernel, n);
 #endif
         case 32: return wavesPerCU<32>(kernel, n);
@@ -1865,7 +1875,7 @@ int persistentWavesPerCU(int stack, int kernel, int& n) {
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
     switch (stack) {
         case 16: launchRender<16>(P, st); break;
-#ifdef PT_STACK24
+#if PT_STACK24
         case 24: launchRender<24>(P, st); break;
 #endif
         case 32: launchRender<32>(P, st); break;
@@ -1882,7 +1892,7 @@ int dispatchTrace(int stack, const DevScene& S, const pt_ray* r, int64_t n, floa
     const unsigned blocks = (unsigned)((n + kWave - 1) / kWave);
     switch (stack) {
         case 16: traceKernel<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
-#ifdef PT_STACK24
+#if PT_STACK24
         case 24: traceKernel<24><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
 #endif
         case 32: traceKernel<32><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
