@@ -502,6 +502,7 @@ struct RenderParams {
     int nblocks, block;
     float* partial;
     unsigned* taskCounter;                    // next task (zeroed before the launch)
+    uint32_t* stackSpill;                     // sample mode, STACK > 32: stack entries >= 32 (per wave slot, lane)
     uint32_t ntasks;                          // tile slots x nblocks x 64
     int nwaves;                               // persistent waves launched
     uint32_t seed0, seed1;
@@ -695,9 +696,14 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 // 5 waves per SIMD (their registers would allow 6, which measured slower: 1,670 vs 1,617 ms)
 template <int STACK>
 constexpr unsigned kCompatPad = STACK * 256 < 8192 ? 8192u - STACK * 256u : 0u;
-template <int STACK, bool SAMPLE>
-constexpr int kWavesPerEU = STACK <= 24 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
-                                        : (STACK <= 32 ? 5 : (STACK <= 48 ? 4 : (STACK <= 64 ? 3 : 2)));
+template <int STACK, bool SAMPLE, bool WIDE>
+constexpr int kLdsStack = (SAMPLE && !WIDE && STACK > 32) ? 32 : STACK;   // entries per lane in LDS
+template <int STACK, bool SAMPLE, bool WIDE>
+constexpr int kWavesPerEU = kLdsStack<STACK, SAMPLE, WIDE> <= 24
+                                ? (SAMPLE ? PT_WAVES_PER_EU : 5)
+                                : (kLdsStack<STACK, SAMPLE, WIDE> <= 32
+                                       ? 5
+                                       : (kLdsStack<STACK, SAMPLE, WIDE> <= 48 ? 4 : (STACK <= 64 ? 3 : 2)));
 
 // One NODE step on the 4-wide tree for one lane.  Entries of a wide node are in the reference's
 // DFS order: leading hit leaves go to the leaf queue (with their entry distance), the first hit
@@ -794,8 +800,11 @@ __device__ __forceinline__ void wideNodeStep(const DevScene& S, int& node, int& 
 // slab entry distance; leaves that wait on the stack behind an internal entry are queued with
 // lo = -inf and re-tested exactly from the primitive's vertices (primBoxHit).
 template <int STACK, bool SAMPLE, bool WIDE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE>))) void renderKernelWF(RenderParams P) {
-    __shared__ uint32_t stk[STACK * kWave];
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
+    // Sample mode on deep trees keeps 32 stack entries per lane in LDS (8 KB per wave: 5 waves per
+    // SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
+    constexpr int LS = kLdsStack<STACK, SAMPLE, WIDE>;
+    __shared__ uint32_t stk[LS * kWave];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1078,13 +1087,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 // No overflow check: an entry is pushed only for a left sibling on the current
                 // path, one per level, so sp < depth <= STACK - 1 (stackFor).
                 if (ir) {
-                    if (il) { my[sp * kWave] = lref; sp++; }
+                    if (il) {
+                        if (LS == STACK || sp < LS) my[sp * kWave] = lref;
+                        else P.stackSpill[((size_t)blockIdx.x * kWave + lane) * (STACK - LS) + (sp - LS)] = lref;
+                        sp++;
+                    }
                     node = (int)rref;
                 } else if (il) {
                     node = (int)lref;
                 } else if (sp > 0) {
                     sp--;
-                    node = (int)my[sp * kWave];
+                    node = (LS == STACK || sp < LS)
+                               ? (int)my[sp * kWave]
+                               : (int)P.stackSpill[((size_t)blockIdx.x * kWave + lane) * (STACK - LS) + (sp - LS)];
                 } else {
                     node = -1;
                 }
@@ -1736,6 +1751,7 @@ struct pt_film {
     std::vector<unsigned> cost;   // host copy of tileCost and the spp it was measured at
     int costSpp = 0;
     DevBuf partial, taskCounter;  // sample mode: per-block partial sums; task counter
+    DevBuf stackSpill;            // sample mode on deep trees: traversal stack entries beyond LDS
     size_t partialBytes = 0;
     DevBuf sums;                  // compat mode: raw per-pixel sample sums of the frame (resolve input)
     DevBuf accum;                 // progressive rendering: fp32 RGB running sums of every accumulated frame
@@ -2379,6 +2395,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.block = 0;
     P.partial = nullptr;
     P.taskCounter = nullptr;
+    P.stackSpill = nullptr;
     P.ntasks = 0;
     P.nwaves = 0;
     P.seed0 = (uint32_t)f->seed;
@@ -2430,6 +2447,10 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
+        if (kernel == PT_KERNEL_WAVEFRONT && stack > 32) {   // kLdsStack: entries 32.. in global memory
+            if ((rc = devReserve(f->stackSpill, (size_t)P.nwaves * kWave * (size_t)(stack - 32) * 4))) return rc;
+            P.stackSpill = f->stackSpill.as<uint32_t>();
+        }
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
     }
     // A resolve pass follows the render kernel in sample mode (block sums) and whenever the film

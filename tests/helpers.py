@@ -90,3 +90,54 @@ def read_png(path):
     raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 4 * w)
     assert (raw[:, 0] == 0).all()
     return raw[:, 1:].reshape(h, w, 4)
+
+
+def deep_stack_scene(n_group: int = 2048, L: float = 2048.0):
+    """Spheres whose LBVH makes a traversal stack deeper than 32 entries (the sample-mode kernel
+    keeps 32 per lane in LDS and the rest in global memory).  Every sphere's box contains the
+    point (L/2, L/2, L/2), so a ray starting there hits every box and visits the whole tree.
+    Morton cells are placed exactly: with radius r = L/2 and anchors at 0 and L the scene box is
+    [-r, L + r] and cell = (c + r) / 4 for L = 2048.  A group of n_group spheres in cell
+    (511, 511, 511) (27 one-bits in its code), plus a pair per low cell bit with that bit cleared:
+    each pair is an internal left sibling on the path to the group (one push per pair), and the
+    group's object-id bits add ~log2(n_group) more."""
+    r = L / 2
+
+    def centre(cell):
+        return 4.0 * cell - r + 2.0
+
+    g = 511
+    cells = []
+    for axis in range(3):
+        for b in range(8):
+            c = [g, g, g]
+            c[axis] = g & ~(1 << b)
+            cells += [c, c]
+    cells += [[g, g, g]] * n_group
+    objs = np.zeros(len(cells) + 2, OBJECT_DTYPE)
+    objs["type"] = 1
+    objs["mat"] = 0
+    objs["v"][:len(cells), :3] = [[centre(x) for x in c] for c in cells]
+    objs["v"][len(cells), :3] = 0.0
+    objs["v"][len(cells) + 1, :3] = L
+    objs["v"][:, 3] = r
+    mats = np.zeros(1, MATERIAL_DTYPE)
+    mats["type"] = 1
+    mats["albedo"] = (0.5, 0.6, 0.7)
+    return objs, mats
+
+
+def max_stack(nodes: np.ndarray, n: int) -> int:
+    """Deepest traversal stack (push left, descend right) when every box is hit."""
+    best, todo = 0, [(0, 0)]
+    while todo:
+        i, d = todo.pop()
+        best = max(best, d)
+        left, right = nodes["left"][i], nodes["right"][i]
+        li, ri = left < n - 1, right < n - 1
+        if ri:
+            todo.append((right, d + (1 if li else 0)))
+        if li:
+            todo.append((left, d))
+    return best
+
