@@ -696,8 +696,11 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 // 5 waves per SIMD (their registers would allow 6, which measured slower: 1,670 vs 1,617 ms)
 template <int STACK>
 constexpr unsigned kCompatPad = STACK * 256 < 8192 ? 8192u - STACK * 256u : 0u;
+#ifndef PT_LDS_STACK
+#define PT_LDS_STACK 32   // sample mode: traversal stack entries per lane kept in LDS
+#endif
 template <int STACK, bool SAMPLE, bool WIDE>
-constexpr int kLdsStack = (SAMPLE && !WIDE && STACK > 32) ? 32 : STACK;   // entries per lane in LDS
+constexpr int kLdsStack = (SAMPLE && !WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kWavesPerEU = kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
@@ -2447,8 +2450,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
-        if (kernel == PT_KERNEL_WAVEFRONT && stack > 32) {   // kLdsStack: entries 32.. in global memory
-            if ((rc = devReserve(f->stackSpill, (size_t)P.nwaves * kWave * (size_t)(stack - 32) * 4))) return rc;
+        if (kernel == PT_KERNEL_WAVEFRONT && stack > PT_LDS_STACK) {   // kLdsStack: the rest in memory
+            if ((rc = devReserve(f->stackSpill, (size_t)P.nwaves * kWave * (size_t)(stack - PT_LDS_STACK) * 4)))
+                return rc;
             P.stackSpill = f->stackSpill.as<uint32_t>();
         }
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
