@@ -700,7 +700,7 @@ constexpr unsigned kCompatPad = STACK * 256 < 8192 ? 8192u - STACK * 256u : 0u;
 #define PT_LDS_STACK 32   // sample mode: traversal stack entries per lane kept in LDS
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
-constexpr int kLdsStack = (SAMPLE && !WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
+constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kWavesPerEU = kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
@@ -804,8 +804,8 @@ __device__ __forceinline__ void wideNodeStep(const DevScene& S, int& node, int& 
 // lo = -inf and re-tested exactly from the primitive's vertices (primBoxHit).
 template <int STACK, bool SAMPLE, bool WIDE>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
-    // Sample mode on deep trees keeps 32 stack entries per lane in LDS (8 KB per wave: 5 waves per
-    // SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
+    // Deep trees (binary kernels) keep 32 stack entries per lane in LDS (8 KB per wave: 5 waves
+    // per SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
     constexpr int LS = kLdsStack<STACK, SAMPLE, WIDE>;
     __shared__ uint32_t stk[LS * kWave];
     const int lane = threadIdx.x;
@@ -2450,12 +2450,15 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
-        if (kernel == PT_KERNEL_WAVEFRONT && stack > PT_LDS_STACK) {   // kLdsStack: the rest in memory
-            if ((rc = devReserve(f->stackSpill, (size_t)P.nwaves * kWave * (size_t)(stack - PT_LDS_STACK) * 4)))
-                return rc;
-            P.stackSpill = f->stackSpill.as<uint32_t>();
-        }
+
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
+    }
+    // Deep trees: stack entries beyond kLdsStack live in memory, per wave slot (persistent wave or
+    // compat tile) and lane
+    if (kernel == PT_KERNEL_WAVEFRONT && stack > PT_LDS_STACK && P.ntiles > 0) {
+        const size_t slots = sample ? (size_t)P.nwaves : (size_t)P.ntiles;
+        if ((rc = devReserve(f->stackSpill, slots * kWave * (size_t)(stack - PT_LDS_STACK) * 4))) return rc;
+        P.stackSpill = f->stackSpill.as<uint32_t>();
     }
     // A resolve pass follows the render kernel in sample mode (block sums) and whenever the film
     // accumulates or the output is 8-bit; compat kernels then store raw sums into f->sums.
