@@ -490,6 +490,7 @@ struct RenderParams {
     int spp, max_depth;
     float invW, invH, invSpp;
     int leafBatch, shadeBatch;                // wavefront scheduler thresholds (lanes)
+    int nodeMin;                              // compat: below this many NODE lanes, run the larger of LEAF / SHADE
     int kernel;                               // PT_KERNEL_*
     unsigned long long* waveTimes;            // optional (PT_WAVE_TIMES): {start, end, tile|xcc<<32} per wave
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
@@ -1025,6 +1026,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         if (nN == 0) kind = nL > 0 ? 1 : 2;
         else if (nL >= P.leafBatch) kind = 1;
         else if (nS >= P.shadeBatch) kind = 2;
+        else if (!SAMPLE && nN < P.nodeMin && (nL | nS)) kind = nL >= nS ? 1 : 2;
         else kind = 0;
 #ifdef PT_DIAG
         const unsigned long long tK0 = __builtin_amdgcn_s_memtime();
@@ -2410,6 +2412,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     const bool sampleRng = rng == PT_RNG_SAMPLE;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
                                                  : envInt("PT_LEAF_BATCH", sampleRng ? 24 : 8);
+    // compat mode: a NODE step with fewer than nodeMin lanes yields to the larger of the waiting
+    // LEAF / SHADE groups (C3 compat 1,620 -> 1,517 ms at 8; 4: 1,548, 16: 1,671, 32: 1,989)
+    P.nodeMin = std::getenv("PT_NODE_MIN") ? std::atoi(std::getenv("PT_NODE_MIN")) : 8;
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
                                                    : envInt("PT_SHADE_BATCH", sampleRng ? 32 : 12);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
