@@ -2405,13 +2405,13 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.nwaves = 0;
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
-    // Defaults swept on C3 (tools/gpu_variants.sh): compat mode is bound by its slowest pixels'
-    // sequential chains, so lanes must not wait long (8 / 12; frame times vary by ±5 %);
-    // sample mode is throughput-bound and prefers fuller LEAF / SHADE steps (24 / 32: 1,741 ->
-    // 1,326..1,355 ms).
+    // Defaults swept on C3 (tools/gpu_variants.sh): sample mode is throughput-bound and prefers
+    // full LEAF / SHADE steps (24 / 32: 1,741 -> 1,326..1,355 ms when introduced).  Compat mode
+    // is bound by its slowest pixels' sequential chains: 20 / 12 together with nodeMin 8 (C3
+    // 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 -> 1,180 against 8 / 12).
     const bool sampleRng = rng == PT_RNG_SAMPLE;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
-                                                 : envInt("PT_LEAF_BATCH", sampleRng ? 24 : 8);
+                                                 : envInt("PT_LEAF_BATCH", sampleRng ? 24 : 20);
     // compat mode: a NODE step with fewer than nodeMin lanes yields to the larger of the waiting
     // LEAF / SHADE groups (C3 compat 1,620 -> 1,517 ms at 8; 4: 1,548, 16: 1,671, 32: 1,989)
     P.nodeMin = std::getenv("PT_NODE_MIN") ? std::atoi(std::getenv("PT_NODE_MIN")) : 8;
