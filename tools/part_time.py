@@ -26,7 +26,8 @@ for part in sorted({0, n // 2, n - 1}):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         _, st = ptamd.render(scene, f, p.camera, spp, p.max_depth, out=out.data_ptr(), rng=rng,
-                             flags=ptamd.IDENTITY_ORDER if os.environ.get("IDENTITY") else 0)
+                             flags=ptamd.IDENTITY_ORDER if os.environ.get("IDENTITY") else 0,
+                             chunk=int(os.environ.get("CHUNK", "0")))
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
         kms.append(st.kernel_ms)
