@@ -693,10 +693,15 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 #ifndef PT_STACK24
 #define PT_STACK24 1   // STACK 24 instantiations (C3: depth + 1 <= 24): 6 waves per SIMD fit the LDS
 #endif
-// Compat tile launches on shallow trees: dynamic LDS padding to 8 KB per wave caps them at
-// 5 waves per SIMD (their registers would allow 6, which measured slower: 1,670 vs 1,617 ms)
+// Compat tile launches at STACK 24: dynamic LDS padding to 8 KB per wave caps them at 5 waves
+// per SIMD (their registers would allow 6, which measured slower on C3: 1,491 vs 1,435 ms, whose
+// long per-pixel chains prefer less sharing of each SIMD); STACK 16 (C2, short paths) runs
+// unpadded (73 vs 82 ms)
 template <int STACK>
-constexpr unsigned kCompatPad = STACK * 256 < 8192 ? 8192u - STACK * 256u : 0u;
+#ifndef PT_COMPAT_PAD
+#define PT_COMPAT_PAD 1
+#endif
+constexpr unsigned kCompatPad = (PT_COMPAT_PAD && STACK == 24) ? 8192u - STACK * 256u : 0u;
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 32   // sample mode: traversal stack entries per lane kept in LDS
 #endif
