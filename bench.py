@@ -110,6 +110,9 @@ def main() -> None:
                     help="frame format rendered and gathered: rgba8 (default: quantised on the device like "
                          "PngImage::saveColor, 4 B/pixel on the wire) or f32 (linear-sqrt RGB, 12 B/pixel)")
     ap.add_argument("--png", default="", help="rank 0 writes the last (assembled) frame to this PNG")
+    ap.add_argument("--kernel", default="wide", choices=["wide", "wavefront"],
+                    help="wide (default): the compressed 8-wide SAH tree, nearest child first; wavefront: the "
+                         "binary LBVH in the reference's visiting order.  Same image either way")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -146,7 +149,9 @@ def main() -> None:
 
     sample = args.rng == "sample"
 
-    def frame(kernel=ptamd.KERNEL_DEFAULT):
+    kernel_id = ptamd.KERNEL_WIDE if args.kernel == "wide" else ptamd.KERNEL_WAVEFRONT
+
+    def frame(kernel=kernel_id):
         # every step renders the SAME frame: streams back to curand_init(seed, pixel, 0)
         # (sample mode is stateless: a pure function of seed, pixel and sample)
         if not sample:
@@ -180,10 +185,13 @@ def main() -> None:
     spec_visits = 0
     for _ in range(args.steps):
         st = frame()
-        if st.rays != ref_st.rays or st.tri_tests != ref_st.tri_tests or st.sphere_tests != ref_st.sphere_tests:
-            raise SystemExit("wavefront frame differs from the reference-order frame")
+        if st.rays != ref_st.rays or (args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
+                                                                      st.sphere_tests != ref_st.sphere_tests)):
+            raise SystemExit("frame differs from the reference-order frame")
         rays += st.rays
-        kbytes += ref_st.algo_bytes
+        # algorithmic bytes of the tree the kernel traverses: the wide kernel's own visits; the
+        # binary kernel's reference-order visits (its speculative extra visits are not work)
+        kbytes += st.algo_bytes if args.kernel == "wide" else ref_st.algo_bytes
         spec_visits += st.node_visits
         kms += st.kernel_ms
     torch.cuda.synchronize(dev)
@@ -210,7 +218,8 @@ def main() -> None:
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
             _, cst = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
-                                  stream=stream.cuda_stream, rng=ptamd.RNG_COMPAT, out_format=out_format)
+                                  stream=stream.cuda_stream, rng=ptamd.RNG_COMPAT, out_format=out_format,
+                                  kernel=kernel_id)
             torch.cuda.synchronize(dev)
             el1 = time.perf_counter() - t1
         compat = {"value": cst.rays / el1 / 1e6, "unit": "Mray/s", "ms_per_step": el1 * 1e3,

@@ -143,6 +143,10 @@ int pt_scene_download_bvh(pt_scene* scene, pt_bvh_node* nodes);
  * rays/hits are host pointers. */
 int pt_trace_closest(pt_scene* scene, const pt_ray* rays, int64_t n, float tmin, float tmax,
                      pt_hit* hits, pt_stats* stats);
+/* pt_trace_closest with a choice of tree: PT_KERNEL_WIDE traverses the compressed 8-wide tree
+ * (see pt_render_ex); any other value the binary LBVH in the reference's order.  Same hits. */
+int pt_trace_closest_ex(pt_scene* scene, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel,
+                        pt_hit* hits, pt_stats* stats);
 /* Per-pixel XORWOW streams, initRandom (main.cu:262-269): curand_init(seed, pixel, 0, ...)
  * for every pixel of the rows this film owns.  Rows are grouped in stripes of stripe_height;
  * stripe s belongs to part (s % n_parts).  n_parts = 1 owns the whole frame. */
@@ -162,7 +166,9 @@ int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int
  * kernel: PT_KERNEL_DEFAULT (= PT_KERNEL_WAVEFRONT unless the PT_RENDER_KERNEL environment
  *   variable says "simple" or "wide"), PT_KERNEL_SIMPLE (ray-synchronous, the reference's loop
  *   structure, binary LBVH), PT_KERNEL_WAVEFRONT (per-lane state machine, steps chosen by wave
- *   ballots, binary LBVH) or PT_KERNEL_WIDE (the same on the 4-wide collapse of the LBVH).
+ *   ballots, binary LBVH, the reference's visiting order) or PT_KERNEL_WIDE (the same state
+ *   machine on a compressed 8-wide SAH tree built on the host at first use, nearest child first;
+ *   the closest hit is chosen by (t, the reference's tie order), so the hits are the reference's).
  *   All kernels give bit-identical images for a given rng mode.
  * rng: PT_RNG_COMPAT (default): the reference's semantics -- one cuRAND-XORWOW stream per
  *   pixel, curand_init(seed, pixel, 0), samples consumed in order and kept across calls like

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -28,6 +29,7 @@
 
 #include "../host/pt_error.hpp"
 #include "../host/pt_host.hpp"
+#include "../host/pt_wide8.hpp"
 #include "pt.h"
 
 using pt::fail;
@@ -62,7 +64,11 @@ struct DevScene {
     const float4* prims;     // 3 x float4 per primitive (leaf order)
     const float4* shade;     // 3 x float4 per primitive: {n | c, r} {albedo, fuzz} {ir, type | sphere << 16, mat, obj}
     const float4* mats;      // 2 x float4 per material
-    const float4* wnodes;    // 4-wide nodes, 8 x float4 each (renderKernelWF<.., WIDE>)
+    const float4* wnodes;    // compressed 8-wide nodes, 5 x float4 each (renderKernelWF<.., WIDE>; host/pt_wide8.cpp)
+    const float4* wprims;    // primitive records in wide-tree leaf order, {v0, rank} {v1, objID} {v2, sphere}
+    const float4* wshade;    // shading records in reference rank order (wide kernels)
+    const uint32_t* rankOf;  // leaf k -> its rank in the reference's traversal order
+    const int* iparent;      // parent of each internal LBVH node (-1 for the root)
     unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
     int nprims;
 };
@@ -132,36 +138,11 @@ __device__ __forceinline__ Xorwow sampleStream(uint32_t k0, uint32_t k1, uint32_
 // aabb::hit (aabb.h:21-34): per axis t0=(min-o)*inv, t1=(max-o)*inv, swap if inv<0,
 // tmin=max(tmin,t0), tmax=min(tmax,t1); miss if tmax<tmin.  The ternaries of the reference
 // keep the old bound on NaN, which is exactly maxNum/minNum (v_max_f32 / v_min_f32).
-__device__ __forceinline__ bool slab(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
-                                     float3 o, float3 inv, float tmin, float tmax) {
-    float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
-    float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
-    float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
-    float nx = inv.x < 0.0f ? t1x : t0x, fx = inv.x < 0.0f ? t0x : t1x;
-    float ny = inv.y < 0.0f ? t1y : t0y, fy = inv.y < 0.0f ? t0y : t1y;
-    float nz = inv.z < 0.0f ? t1z : t0z, fz = inv.z < 0.0f ? t0z : t1z;
-    float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
-    float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
-    return !(hi < lo);
-}
-
-// slab() that also returns the entry distance lo = max(tmin, near planes).  For a box that
+// SlabHit also returns the entry distance lo = max(tmin, near planes).  For a box that
 // passed with tmax = T, the same test with any tmax' <= T fails iff tmax' < lo: hi(T') =
 // fminf(T', far planes) and fminf ignores NaN, so hi(T') < lo <=> T' < lo or far < lo, and
 // the latter is false because the box passed.  (lo is never NaN: fmaxf(tmin, NaN) = tmin.)
 struct SlabHit { bool hit; float lo; };
-__device__ __forceinline__ SlabHit slabLo(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
-                                          float3 o, float3 inv, float tmin, float tmax) {
-    float t0x = (mnx - o.x) * inv.x, t1x = (mxx - o.x) * inv.x;
-    float t0y = (mny - o.y) * inv.y, t1y = (mxy - o.y) * inv.y;
-    float t0z = (mnz - o.z) * inv.z, t1z = (mxz - o.z) * inv.z;
-    float nx = inv.x < 0.0f ? t1x : t0x, fx = inv.x < 0.0f ? t0x : t1x;
-    float ny = inv.y < 0.0f ? t1y : t0y, fy = inv.y < 0.0f ? t0y : t1y;
-    float nz = inv.z < 0.0f ? t1z : t0z, fz = inv.z < 0.0f ? t0z : t1z;
-    float lo = fmaxf(fmaxf(fmaxf(tmin, nx), ny), nz);
-    float hi = fminf(fminf(fminf(tmax, fx), fy), fz);
-    return SlabHit{!(hi < lo), lo};
-}
 
 // Internal node record, 16 floats (4 x float4).  Each child box is stored as one (min, max)
 // pair per axis, so every pair sits in an aligned 64-bit register pair and the six slab
@@ -247,29 +228,6 @@ __device__ __forceinline__ Prim loadPrim(const DevScene& S, uint32_t k) {
 #endif
 }
 
-// Exact object box (cuda_object.h:21-42: sphere c -/+ |r|; triangle via utils::unionPoints)
-// tested like aabb::hit: used to re-test a queued leaf against the current closest hit.
-__device__ __forceinline__ bool primBoxHit(const Prim& q, bool sphere, float3 o, float3 inv, float tmin, float tmax) {
-    if (sphere) {
-        const float r = fabsf(q.p1.x);
-        return slab(q.p0.x - r, q.p0.y - r, q.p0.z - r, q.p0.x + r, q.p0.y + r, q.p0.z + r, o, inv, tmin, tmax);
-    }
-    float mnx = q.p0.x, mny = q.p0.y, mnz = q.p0.z, mxx = mnx, mxy = mny, mxz = mnz;
-    if (mnx > q.p1.x) mnx = q.p1.x;
-    if (mny > q.p1.y) mny = q.p1.y;
-    if (mnz > q.p1.z) mnz = q.p1.z;
-    if (mnx > q.p2.x) mnx = q.p2.x;
-    if (mny > q.p2.y) mny = q.p2.y;
-    if (mnz > q.p2.z) mnz = q.p2.z;
-    if (mxx < q.p1.x) mxx = q.p1.x;
-    if (mxy < q.p1.y) mxy = q.p1.y;
-    if (mxz < q.p1.z) mxz = q.p1.z;
-    if (mxx < q.p2.x) mxx = q.p2.x;
-    if (mxy < q.p2.y) mxy = q.p2.y;
-    if (mxz < q.p2.z) mxz = q.p2.z;
-    return slab(mnx, mny, mnz, mxx, mxy, mxz, o, inv, tmin, tmax);
-}
-
 // CudaObj::hit (cuda_object.h:44-92): returns the accepted t (> tmin > 0), or -1 on a miss.
 // `closest` is the current t_max.  Values are returned, never written through references, so
 // the compiler keeps every traversal variable in registers.
@@ -320,6 +278,160 @@ __device__ __forceinline__ void primTest(const DevScene& S, uint32_t ref, float3
     }
 }
 
+// ------------------------------------------------------------------------ wide tree
+// The reference's closest hit does not depend on its traversal order except through ties:
+// a primitive is accepted when t < closest (triangle, cuda_object.h:83) or t <= closest
+// (sphere, :57-61), and its left-first DFS visits leaves in key order k.  So the reference's
+// result over ANY set of visited primitives that contains every primitive it would accept is
+// the minimum of (t, tie rank) with ranks: spheres before triangles, spheres by DESCENDING k
+// (a later sphere at the same t replaces the earlier hit), triangles by ASCENDING k (a later
+// triangle at the same t is rejected).  The wide tree's boxes are conservative (outward-rounded
+// planes, pt_wide8.cpp), so every primitive the reference would accept is visited.
+
+// Candidate distance of a primitive independent of the current closest hit: the sphere's
+// first root when >= tmin, else its second (the reference tries them in this order against
+// [tmin, closest]; the second is never smaller); triangles as primHitT.  -1 on a miss.
+__device__ __forceinline__ float primHitAny(const Prim& q, bool sphere, float3 o, float3 d, float tmin) {
+    if (sphere) {
+        float3 oc = sub(o, xyz(q.p0));
+        float r = q.p1.x;
+        float a = len2(d);
+        float half_b = dot3(oc, d);
+        float cc = len2(oc) - r * r;
+        float disc = half_b * half_b - a * cc;
+        if (disc < 0.0f) return -1.0f;
+        float sq = sqrtf(disc);
+        float root = (-half_b - sq) / a;
+        if (!(root < tmin)) return root;
+        root = (-half_b + sq) / a;
+        if (!(root < tmin)) return root;
+        return -1.0f;
+    }
+    const float3 v0 = xyz(q.p0);
+    float3 e1 = sub(xyz(q.p1), v0), e2 = sub(xyz(q.p2), v0);
+    float3 s1 = cross3(d, e2);
+    float det = dot3(s1, e1);
+    if (det == 0.0f) return -1.0f;
+    float3 s = sub(o, v0);
+    float3 s2 = cross3(s, e1);
+    float inv = 1.0f / det;
+    float t = dot3(s2, e2) * inv;
+    float b1 = dot3(s1, s) * inv;
+    float b2 = dot3(s2, d) * inv;
+    if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 <= 0.0f || b1 + b2 >= 1.0f || t <= tmin)
+        return -1.0f;
+    return t;
+}
+
+// aabb::hit (aabb.h:21-34) on the primitive's exact box (cuda_object.h:21-42: sphere c -/+ |r|,
+// triangle min / max of its vertices): the test the reference's traversal applies to a leaf
+// before its primitive test (render_manager.h:107-123).
+__device__ __forceinline__ SlabHit refLeafBox(const Prim& q, bool sphere, float3 o, float3 inv, float tmin, float tmax) {
+    float mn[3], mx[3];
+    if (sphere) {
+        const float r = fabsf(q.p1.x);
+        mn[0] = q.p0.x - r; mn[1] = q.p0.y - r; mn[2] = q.p0.z - r;
+        mx[0] = q.p0.x + r; mx[1] = q.p0.y + r; mx[2] = q.p0.z + r;
+    } else {
+        mn[0] = mx[0] = q.p0.x; mn[1] = mx[1] = q.p0.y; mn[2] = mx[2] = q.p0.z;
+        const float4 v[2] = {q.p1, q.p2};
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            if (mn[0] > v[i].x) mn[0] = v[i].x;
+            if (mn[1] > v[i].y) mn[1] = v[i].y;
+            if (mn[2] > v[i].z) mn[2] = v[i].z;
+            if (mx[0] < v[i].x) mx[0] = v[i].x;
+            if (mx[1] < v[i].y) mx[1] = v[i].y;
+            if (mx[2] < v[i].z) mx[2] = v[i].z;
+        }
+    }
+    return slabPair(v2f{mn[0], mx[0]}, v2f{mn[1], mx[1]}, v2f{mn[2], mx[2]}, o, inv, tmin, tmax);
+}
+
+// Test wide-order primitive record q ({v0, rank}{v1, obj}{v2, sphere}) and keep the minimum of
+// (t, tie rank).  `best` = rank | kSphereBit for a sphere, -1 before the first hit.
+// The reference only tests a primitive whose exact box passes with the closest hit of that
+// moment (aabb::hit, render_manager.h:107-123; a single primitive is the root and has no box
+// test, :92-98).  A hit inside its own box (entry lo <= t, as exact arithmetic guarantees) is
+// tested by the reference whenever it could matter, in any order.  A grazing hit whose rounded
+// box entry lies beyond it (t < lo) is tested only if the closest hit of that moment is >= lo:
+// the outcome depends on the order exactly when another candidate's t lies in [t, lo).  Such a
+// lane sets `redo` and its query is repeated in the reference's order (traceRefStackless);
+// `bestLo` is the current best's window end (its box entry when t < lo, else -inf).
+__device__ __forceinline__ void wideTest(const Prim& q, float3 o, float3 d, float3 inv, float tmin, float& closest,
+                                         int& best, float& bestLo, bool leafBoxes, bool& redo) {
+    const bool sph = __float_as_uint(q.p2.w) != 0u;
+    const float t = primHitAny(q, sph, o, d, tmin);
+    if (t >= 0.0f) {
+        const int k = (int)__float_as_uint(q.p0.w);
+        const bool none = best < 0, bSph = (best & (int)kSphereBit) != 0;
+        const int bk = best & (int)kPrimMask;
+        const bool tie = sph ? (none || !bSph || k > bk) : (!none && !bSph && k < bk);
+        redo = redo || (t >= closest && t < bestLo);   // not better, but inside the current best's window
+        if (t < closest || (t == closest && tie)) {
+            bool take = true;
+            float lo = -__builtin_inff();
+            if (leafBoxes) {
+                const SlabHit b = refLeafBox(q, sph, o, inv, tmin, __builtin_inff());
+                take = b.hit && !(closest < b.lo);
+                redo = redo || (b.hit && closest < b.lo);   // the current best inside this one's window
+                lo = t < b.lo ? b.lo : lo;
+            }
+            if (take) {
+                closest = t;
+                best = k | (sph ? (int)kSphereBit : 0);
+                bestLo = lo;
+            }
+        }
+    }
+}
+
+// One compressed 8-wide node (five 16-B words, layout in host/pt_wide8.cpp) against the ray:
+// returns the hit mask, internal children in bits 24 + (slot ^ oct), leaf primitives in bits
+// 0..23 (offsets from the node's primitive base).  Plane distances t = q * (s * inv) + (p - o) *
+// inv; the planes lie a quantum outside the exact boxes, far beyond this arithmetic's rounding,
+// and a NaN (0 * inf on an axis the ray is parallel to) only drops that plane: the test never
+// rejects a box the exact slab test (aabb.h:21-34) accepts.
+__device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4 n3, uint4 n4, float3 o, float3 inv,
+                                             uint32_t oct, float tmin, float tmax) {
+    const float ax = __uint_as_float((n0.w & 0xffu) << 23) * inv.x;
+    const float ay = __uint_as_float(((n0.w >> 8) & 0xffu) << 23) * inv.y;
+    const float az = __uint_as_float(((n0.w >> 16) & 0xffu) << 23) * inv.z;
+    const float bx = (__uint_as_float(n0.x) - o.x) * inv.x;
+    const float by = (__uint_as_float(n0.y) - o.y) * inv.y;
+    const float bz = (__uint_as_float(n0.z) - o.z) * inv.z;
+    // near / far planes per axis: qlo for a positive direction, qhi for a negative one
+    const bool sx = (oct & 1u) != 0, sy = (oct & 2u) != 0, sz = (oct & 4u) != 0;
+    const uint32_t nearX[2] = {sx ? n2.z : n2.x, sx ? n2.w : n2.y}, farX[2] = {sx ? n2.x : n2.z, sx ? n2.y : n2.w};
+    const uint32_t nearY[2] = {sy ? n3.z : n3.x, sy ? n3.w : n3.y}, farY[2] = {sy ? n3.x : n3.z, sy ? n3.y : n3.w};
+    const uint32_t nearZ[2] = {sz ? n4.z : n4.x, sz ? n4.w : n4.y}, farZ[2] = {sz ? n4.x : n4.z, sz ? n4.y : n4.w};
+    const uint32_t oct4 = oct * 0x01010101u;
+    uint32_t hits = 0u;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t meta4 = h ? n1.w : n1.z;
+        // per byte: internal children (0b001_11xxx) get their slot bits XOR the ray octant
+        const uint32_t inner4 = (meta4 & (meta4 << 1)) & 0x10101010u;
+        const uint32_t innerMask4 = ((inner4 << 3) >> 7) * 0xffu;
+        const uint32_t bitIndex4 = (meta4 ^ (oct4 & innerMask4)) & 0x1f1f1f1fu;
+        const uint32_t childBits4 = (meta4 >> 5) & 0x07070707u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const float tnx = __builtin_fmaf((float)((nearX[h] >> (8 * j)) & 0xffu), ax, bx);
+            const float tny = __builtin_fmaf((float)((nearY[h] >> (8 * j)) & 0xffu), ay, by);
+            const float tnz = __builtin_fmaf((float)((nearZ[h] >> (8 * j)) & 0xffu), az, bz);
+            const float tfx = __builtin_fmaf((float)((farX[h] >> (8 * j)) & 0xffu), ax, bx);
+            const float tfy = __builtin_fmaf((float)((farY[h] >> (8 * j)) & 0xffu), ay, by);
+            const float tfz = __builtin_fmaf((float)((farZ[h] >> (8 * j)) & 0xffu), az, bz);
+            const float lo = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), tmin);
+            const float hi = fminf(fminf(fminf(tfx, tfy), tfz), tmax);
+            const uint32_t bits = ((childBits4 >> (8 * j)) & 0xffu) << ((bitIndex4 >> (8 * j)) & 0xffu);
+            hits |= lo <= hi ? bits : 0u;
+        }
+    }
+    return hits;
+}
+
 // RenderManager::hitBvh (render_manager.h:86-135): same visiting order (left child, right
 // child, leaf children tested at once, internal children pushed left then right).
 // Returns the leaf slot of the closest hit or -1; `closest` holds its t.
@@ -359,19 +471,69 @@ __device__ __forceinline__ int trace(const DevScene& S, float3 o, float3 d, floa
     return best;
 }
 
+// RenderManager::hitBvh (render_manager.h:86-135) without a stack, for the wide kernels' rare
+// order-dependent queries: the same primitive tests in the same order with the same `closest`.
+// The reference pushes an internal child when its box passes at the parent's visit and pops
+// right before left; here a child is entered when its box passes at the moment it would be
+// popped (parent links lead back up).  A box that passed earlier but fails now has children
+// that all fail now (their boxes are inside it; correctly rounded slab arithmetic is monotonic),
+// so skipping it changes no primitive test.  Returns the leaf k of the closest hit or -1.
+__device__ __forceinline__ int traceRefStackless(const DevScene& S, float3 o, float3 d, float tmin, float& closest) {
+    int best = -1;
+    if (S.nprims <= 0) return -1;
+    if (S.nprims == 1) {   // root is a leaf: tested without a box test (:92-98)
+        const float t1 = primHitT(loadPrim(S, 0), __float_as_uint(S.prims[2].w) != 0, o, d, tmin, closest);
+        if (t1 >= 0.0f) { closest = t1; best = 0; }
+        return best;
+    }
+    const float3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    int node = 0, from = -1;   // from >= 0: returning from that child of `node`
+    for (int guard = 0; guard <= 2 * S.nprims; guard++) {
+        const float4* np = S.nodes + 4 * (size_t)node;
+        const float4 a = np[0], b = np[1], q = np[2], r = np[3];
+        const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
+        int next = -1;
+        if (from < 0) {   // visit: the leaf children in order, then the right subtree, then the left
+            const SlabHit hl = slabLeft(a, b, o, inv, tmin, closest);
+            if (hl.hit && (lref & kLeafBit)) {
+                const float t = primHitT(loadPrim(S, lref & kPrimMask), (lref & kSphereBit) != 0, o, d, tmin, closest);
+                if (t >= 0.0f) { closest = t; best = (int)(lref & kPrimMask); }
+            }
+            const SlabHit hr = slabRight(b, q, o, inv, tmin, closest);
+            if (hr.hit && (rref & kLeafBit)) {
+                const float t = primHitT(loadPrim(S, rref & kPrimMask), (rref & kSphereBit) != 0, o, d, tmin, closest);
+                if (t >= 0.0f) { closest = t; best = (int)(rref & kPrimMask); }
+            }
+            if (hr.hit && !(rref & kLeafBit)) next = (int)rref;
+            else if (!(lref & kLeafBit) && slabLeft(a, b, o, inv, tmin, closest).hit) next = (int)lref;
+        } else if ((uint32_t)from == rref && !(lref & kLeafBit) && slabLeft(a, b, o, inv, tmin, closest).hit) {
+            next = (int)lref;
+        }
+        if (next >= 0) {
+            node = next;
+            from = -1;
+        } else {
+            if (node == 0) break;
+            from = node;
+            node = S.iparent[node];
+        }
+    }
+    return best;
+}
+
 // Hit record for leaf slot k at distance t (cuda_object.h:62-67 / 85-88, hit_record.h:21-24),
 // with the hit object's material (material.h:17-68) carried along: the three independent 16-B
 // loads of the shading record are one memory round trip (instead of prim -> normal -> material).
 struct HitRec { float3 p, n; int mat, obj; bool front; float4 m0; float ir; int type; };
 
-__device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, float3 o, float3 d) {
+__device__ __forceinline__ HitRec makeHitFrom(const float4* shade, int k, float t, float3 o, float3 d) {
     HitRec h;
 #if PT_BUFFER_LOADS
-    const __amdgpu_buffer_rsrc_t rs = rawRsrc(S.shade);
+    const __amdgpu_buffer_rsrc_t rs = rawRsrc(shade);
     const uint32_t off = (uint32_t)k * 48u;
     const float4 s0 = bload4(rs, off), s1 = bload4(rs, off + 16u), s2 = bload4(rs, off + 32u);
 #else
-    const float4* r = S.shade + 3 * (size_t)k;
+    const float4* r = shade + 3 * (size_t)k;
     const float4 s0 = r[0], s1 = r[1], s2 = r[2];
 #endif
     const uint32_t tf = __float_as_uint(s2.y);
@@ -390,6 +552,9 @@ __device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, flo
     h.ir = s2.x;
     h.type = (int)(tf & 0xffffu);
     return h;
+}
+__device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, float3 o, float3 d) {
+    return makeHitFrom(S.shade, k, t, o, d);
 }
 
 // ------------------------------------------------------------------------ BSDFs
@@ -669,9 +834,6 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #ifndef PT_LEAF_QUEUE_SAMPLE
 #define PT_LEAF_QUEUE_SAMPLE 2   // sample mode, binary tree, STACK <= 32; compat prefers 4 (C3 1774 vs 1959 ms)
 #endif
-#ifndef PT_WIDE_EXACT
-#define PT_WIDE_EXACT 0   // debug: re-test every wide-tree leaf from its vertices
-#endif
 #ifndef PT_LEAF_PREFETCH
 #define PT_LEAF_PREFETCH 1
 #endif
@@ -693,121 +855,26 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 #ifndef PT_STACK24
 #define PT_STACK24 1   // STACK 24 instantiations (C3: depth + 1 <= 24): 6 waves per SIMD fit the LDS
 #endif
-// Compat tile launches at STACK 24: dynamic LDS padding to 8 KB per wave caps them at 5 waves
-// per SIMD (their registers would allow 6, which measured slower on C3: 1,491 vs 1,435 ms, whose
-// long per-pixel chains prefer less sharing of each SIMD); STACK 16 (C2, short paths) runs
-// unpadded (73 vs 82 ms)
-template <int STACK>
-#ifndef PT_COMPAT_PAD
-#define PT_COMPAT_PAD 1
-#endif
-constexpr unsigned kCompatPad = (PT_COMPAT_PAD && STACK == 24) ? 8192u - STACK * 256u : 0u;
 #ifndef PT_LDS_STACK
 #define PT_LDS_STACK 32   // sample mode: traversal stack entries per lane kept in LDS
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
+#ifndef PT_WIDE_WAVES_PER_EU
+#define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
+#endif
 template <int STACK, bool SAMPLE, bool WIDE>
-constexpr int kWavesPerEU = kLdsStack<STACK, SAMPLE, WIDE> <= 24
+constexpr int kWavesPerEU = WIDE ? PT_WIDE_WAVES_PER_EU : kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
                                 : (kLdsStack<STACK, SAMPLE, WIDE> <= 32
                                        ? 5
                                        : (kLdsStack<STACK, SAMPLE, WIDE> <= 48 ? 4 : (STACK <= 64 ? 3 : 2)));
 
-// One NODE step on the 4-wide tree for one lane.  Entries of a wide node are in the reference's
-// DFS order: leading hit leaves go to the leaf queue (with their entry distance), the first hit
-// internal entry is visited next, the hit entries after it are pushed in reverse order; with no
-// internal entry to descend into, stack tops are popped (leaves into the queue) until an internal
-// node, an empty stack or a full queue (node = -2: continue when the queue has room).
-template <int STACK>
-__device__ __forceinline__ void wideNodeStep(const DevScene& S, int& node, int& sp, int& qn, uint32_t (&qref)[kLeafQ],
-                                             float (&lq)[kLeafQ], uint32_t* my, float3 o, float3 inv,
-                                             float closest) {
-    bool needPop = node == -2;
-    if (node >= 0) {
-        const float4* np = S.wnodes + 8 * (size_t)node;
-        const float4 mnx = np[0], mny = np[1], mnz = np[2], mxx = np[3], mxy = np[4], mxz = np[5];
-        const float4 rf = np[6];
-        const SlabHit h0 = slabLo(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, inv, 0.001f, closest);
-        const SlabHit h1 = slabLo(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, inv, 0.001f, closest);
-        const SlabHit h2 = slabLo(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, inv, 0.001f, closest);
-        const SlabHit h3 = slabLo(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, inv, 0.001f, closest);
-        int mask = (h0.hit ? 1 : 0) | (h1.hit ? 2 : 0) | (h2.hit ? 4 : 0) | (h3.hit ? 8 : 0);
-        const uint32_t refs[4] = {__float_as_uint(rf.x), __float_as_uint(rf.y), __float_as_uint(rf.z),
-                                  __float_as_uint(rf.w)};
-        const float los[4] = {h0.lo, h1.lo, h2.lo, h3.lo};
-        int next = -1;
-        bool full = false;
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            if (next < 0 && !full && ((mask >> e) & 1)) {
-                const uint32_t ref = refs[e];
-                if (ref & kLeafBit) {
-                    if (qn < kLeafQ) {
-#pragma unroll
-                        for (int i = 0; i < kLeafQ; i++) {
-                            qref[i] = qn == i ? ref : qref[i];
-                            lq[i] = qn == i ? (PT_WIDE_EXACT ? -__builtin_inff() : los[e]) : lq[i];
-                        }
-                        qn++;
-                        mask &= ~(1 << e);
-                    } else {
-                        full = true;
-                    }
-                } else {
-                    next = (int)ref;
-                    mask &= ~(1 << e);
-                }
-            }
-        }
-#pragma unroll
-        for (int e = 3; e >= 0; e--) {
-            if ((mask >> e) & 1) {
-                if (sp < STACK) { my[sp * kWave] = refs[e]; sp++; }
-                else { atomicOr(S.err, 2u); }
-            }
-        }
-        if (next >= 0) node = next;
-        else if (full) node = -2;
-        else needPop = true;
-    }
-    if (needPop) {   // pop stacked leaves into the queue until an internal node (bounded)
-        node = -1;
-        bool decided = false;
-#pragma unroll
-        for (int it = 0; it < 4; it++) {
-            if (!decided) {
-                if (sp == 0) {
-                    decided = true;
-                } else {
-                    const uint32_t e = my[(sp - 1) * kWave];
-                    if (!(e & kLeafBit)) {
-                        node = (int)e;
-                        sp--;
-                        decided = true;
-                    } else if (qn < kLeafQ) {
-#pragma unroll
-                        for (int i = 0; i < kLeafQ; i++) {
-                            qref[i] = qn == i ? e : qref[i];
-                            lq[i] = qn == i ? -__builtin_inff() : lq[i];
-                        }
-                        qn++;
-                        sp--;
-                    } else {
-                        node = -2;
-                        decided = true;
-                    }
-                }
-            }
-        }
-        if (!decided) node = sp > 0 ? -2 : -1;
-    }
-}
-
-// WIDE: traverse the 4-wide collapse of the LBVH (wnodes; layout and entry order above traceKernel);
-// a ray needs about half the dependent NODE steps.  Leaves reached directly are queued with their
-// slab entry distance; leaves that wait on the stack behind an internal entry are queued with
-// lo = -inf and re-tested exactly from the primitive's vertices (primBoxHit).
+// WIDE: traverse the compressed 8-wide tree (wnodes / wprims, host/pt_wide8.cpp) instead of the
+// binary LBVH.  Per lane: a node group `ng` (child base << 8 | hit internal slots, in slot ^ oct
+// order, the nearest first), a primitive group (tgBase, tg = hit leaf primitives); NODE takes the
+// next child of the group (pushing the rest), LEAF tests up to two primitives, keeping the
+// minimum (t, tie rank) of wideTest -- the reference's closest hit, in any visiting order.
 template <int STACK, bool SAMPLE, bool WIDE>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
     // Deep trees (binary kernels) keep 32 stack entries per lane in LDS (8 KB per wave: 5 waves
@@ -835,14 +902,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     const DevScene& S = P.S;
 #if PT_NODE_BUFFER_LOADS
     // gfx9 buffer resource: base = the node array, raw (stride 0), DATA_FORMAT_32 in dword 3
-    const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(S.nodes);
+    const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(WIDE ? (const void*)S.wnodes : (const void*)S.nodes);
 #endif
     uint32_t* my = stk + lane;
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
 #ifdef PT_DIAG
-    uint32_t itN = 0, itL = 0, itS = 0, sPops = 0;   // scheduler diagnostics (iterations per kind)
+    uint32_t itN = 0, itL = 0, itS = 0, sPops = 0, sRedo = 0;   // scheduler diagnostics (iterations per kind)
     unsigned long long cycN = 0, cycL = 0, cycS = 0;   // and shader cycles per kind
     unsigned long long cycSh = 0, cycTk = 0, cycNp = 0, cycBr = 0;   // SHADE: shading, tasks, new path, ray start
 #define PT_DIAG_ADD(v, x) (v) += (x)
@@ -866,6 +933,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     float lq[LQ];     // their slab entry distances
 #pragma unroll
     for (int i = 0; i < LQ; i++) { qref[i] = 0u; lq[i] = 0.0f; }
+    // wide tree traversal state (WIDE): node group, primitive group, ray octant (| 8: redo the
+    // query in the reference's order), the best hit's window end
+    uint32_t ng = 0u, tgBase = 0u, tg = 0u, oct = 0u;
+    float bestLo = 0.0f;
     bool active = false;
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
     uint32_t taskRays = 0, depthPaths = 0;
@@ -882,7 +953,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         best = -1;                                                                                \
         sp = 0;                                                                                   \
         qn = 0;                                                                                   \
-        if (S.nprims <= 1) {                                                                      \
+        if constexpr (WIDE) {   /* the root is slot 0 of a virtual node at base 0 */              \
+            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
+            oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);  \
+            tg = 0u;                                                                              \
+            bestLo = -__builtin_inff();                                                           \
+            ng = S.nprims > 0 ? (1u << oct) : 0u;                                                 \
+        } else if (S.nprims <= 1) {                                                               \
             node = -1;                                                                            \
             if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
                 const float t1 = primHitT(loadPrim(S, 0), __float_as_uint(S.prims[2].w) != 0, o, d, \
@@ -1021,9 +1098,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     for (;;) {
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
-        const bool wantNode = WIDE ? (node >= 0 || (node == -2 && qn < LQ)) : (node >= 0 && qn <= LQ - 2);
-        const bool wantLeaf = qn > 0;
-        const bool wantShade = (active && node == -1 && qn == 0) || needTask;   // (-2: wide stack top pending)
+        // binary: room for both children's leaves in the queue; wide: no primitives pending
+        const bool wantNode = WIDE ? (tg == 0u && ((ng & 0xffu) != 0u || sp > 0)) : (node >= 0 && qn <= LQ - 2);
+        const bool wantLeaf = WIDE ? tg != 0u : qn > 0;
+        const bool wantShade = (active && (WIDE ? (tg == 0u && (ng & 0xffu) == 0u && sp == 0) : (node == -1 && qn == 0))) ||
+                               needTask;
         const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
@@ -1042,7 +1121,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             sVisits += (uint32_t)nN;
             PT_DIAG_ADD(itN, 1u);
             if constexpr (WIDE) {
-                if (wantNode) wideNodeStep<STACK>(S, node, sp, qn, qref, lq, my, o, inv, closest);
+                if (wantNode) {
+                    if ((ng & 0xffu) == 0u) { sp--; ng = my[sp * kWave]; }   // the group below
+                    const uint32_t bit = (uint32_t)__builtin_ctz(ng & 0xffu);   // nearest remaining child
+                    const uint32_t child = (ng >> 8) + (bit ^ (oct & 7u));
+                    ng &= ~(1u << bit);
+                    if (ng & 0xffu) { my[sp * kWave] = ng; sp++; }   // sp < depth <= STACK (host check)
+                    const uint32_t off = child * 80u;
+                    const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+                    const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+                    const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+                    const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+                    const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+                    const uint32_t hits = wideHits(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
+                    ng = (n1.x << 8) | (hits >> 24);
+                    tgBase = n1.y;
+                    tg = hits & 0xffffffu;
+                }
             } else if (wantNode) {
 #if PT_NODE_BUFFER_LOADS
                 // buffer loads: a 32-bit per-lane offset off a wave-uniform resource (no 64-bit
@@ -1120,6 +1215,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             bool tested = false, sph = false;
             PT_DIAG_ADD(itL, 1u);
             PT_DIAG_ADD(sPops, (uint32_t)nL);
+            if constexpr (WIDE) {
+                // up to two primitives of the group per step, both records loaded up front
+                uint32_t k0 = 0u, k1 = 0u;
+                const bool h0 = tg != 0u;
+                if (h0) { k0 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
+                const bool h1 = tg != 0u;
+                if (h1) { k1 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
+                const float4* w0 = S.wprims + 3 * (size_t)k0;
+                const float4* w1 = S.wprims + 3 * (size_t)k1;
+                Prim q0{}, q1{};
+                if (h0) q0 = Prim{w0[0], w0[1], w0[2]};
+                if (h1) q1 = Prim{w1[0], w1[1], w1[2]};
+                bool redo = false;
+                if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                if (h1) wideTest(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
+                const bool s0 = __float_as_uint(q0.p2.w) != 0u, s1 = __float_as_uint(q1.p2.w) != 0u;
+                sTris += (uint32_t)__popcll(__ballot(h0 && !s0)) + (uint32_t)__popcll(__ballot(h1 && !s1));
+                sSph += (uint32_t)__popcll(__ballot(h0 && s0)) + (uint32_t)__popcll(__ballot(h1 && s1));
+            } else {
             // Every lane tests all of its queued leaves, in order, in this step (the queue then
             // is empty and the lane rejoins NODE steps; measured -4 % vs one leaf per step).
             // The first two queued primitives are loaded together up front (their addresses are
@@ -1153,7 +1268,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #endif
                     // (wide: a leaf that waited on the stack has no entry distance, lo = -inf:
                     // exact re-test of its box from the primitive's vertices)
-                    if (!(WIDE && lo == -__builtin_inff()) || primBoxHit(pr, sph, o, inv, 0.001f, closest)) {
+                    {
                         tested = true;
                         const float t = primHitT(pr, sph, o, d, 0.001f, closest);
                         if (t >= 0.0f) { closest = t; best = (int)k; }
@@ -1163,19 +1278,28 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             sTris += (uint32_t)__popcll(__ballot(tested && !sph));
             sSph += (uint32_t)__popcll(__ballot(tested && sph));
             }
+            }
         }
         if (kind == 2) {
             // ------------------------------------------------------------------ SHADE
             bool newRay = false, newSample = false;
             PT_DIAG_ADD(itS, 1u);
+            if constexpr (WIDE) PT_DIAG_ADD(sRedo, (uint32_t)__popcll(__ballot(wantShade && !needTask && (oct & 8u))));
             if (wantShade && !needTask) {
                 bool done = false;
                 float3 contrib = f3(0.0f, 0.0f, 0.0f);
+                if constexpr (WIDE) {
+                    if (oct & 8u) {   // rare: the query in the reference's order (ranks index wshade)
+                        closest = __builtin_inff();
+                        const int k = traceRefStackless(S, o, d, 0.001f, closest);
+                        best = k >= 0 ? (int)S.rankOf[k] : -1;
+                    }
+                }
                 if (best < 0) {
                     contrib = sky(d, att);
                     done = true;
                 } else {
-                    HitRec h = makeHit(S, best, closest, o, d);
+                    HitRec h = WIDE ? makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d) : makeHit(S, best, closest, o, d);
                     float3 na;
                     if (!scatter(S, h, d, na, g)) {
                         done = true;
@@ -1270,6 +1394,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         atomicAdd(P.counters + 17, cycTk);
         atomicAdd(P.counters + 18, cycNp);
         atomicAdd(P.counters + 19, cycBr);
+        atomicAdd(P.counters + 20, (unsigned long long)sRedo);
 #endif
     }
 }
@@ -1340,14 +1465,7 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
     static_cast<uint32_t*>(out)[i] = px;
 }
 
-// The 4-wide tree (renderKernelWF<.., WIDE = true>).  Wide node (128 B = 8 x float4): SoA child boxes
-// {minx[4]}{miny[4]}{minz[4]}{maxx[4]}{maxy[4]}{maxz[4]}, {ref[4]}, pad.  A wide node is a
-// two-level collapse of the reference LBVH node N whose entries are listed in the reference's
-// DFS order: [L if leaf][R if leaf] + expand(R) + expand(L), expand(X) = [XL if leaf][XR if
-// leaf][XR if internal][XL if internal].  Testing an entry's box directly instead of its
-// skipped binary ancestor's is exact (the entry box is inside the ancestor box: the slab
-// interval can only shrink), and leaves keep the exact re-test, so every pixel is identical to
-// the reference order; a ray needs about half the dependent node steps.
+// pt_trace_closest on the binary LBVH, in the reference order (trace<STACK>).
 template <int STACK>
 __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* rays, int64_t n, float tmin,
                                                      float tmax, pt_hit* hits, unsigned long long* counters) {
@@ -1375,6 +1493,89 @@ __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* r
             h.n[0] = hr.n.x; h.n[1] = hr.n.y; h.n[2] = hr.n.z;
         }
         hits[i] = h;
+    }
+    waveReduceAdd(counters + 0, c.rays);
+    waveReduceAdd(counters + 1, c.visits);
+    waveReduceAdd(counters + 2, c.tris);
+    waveReduceAdd(counters + 3, c.spheres);
+}
+
+// pt_trace_closest on the wide tree (PT_KERNEL_WIDE): the same traversal as renderKernelWF's
+// WIDE steps, one lane per ray, the same hit records as traceKernel.
+template <int STACK>
+__global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ray* rays, int64_t n, float tmin,
+                                                         float tmax, pt_hit* hits, unsigned long long* counters) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kWave + lane;
+    uint32_t* my = stk + lane;
+    const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(S.wnodes);
+    Counters c{0, 0, 0, 0};
+    if (i < n) {
+        const pt_ray r = rays[i];
+        const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
+        const float3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+        float closest = tmax;
+        int best = -1, sp = 0;
+        bool redo = false;
+        float bestLo = -__builtin_inff();
+        uint32_t ng = S.nprims > 0 ? (1u << oct) : 0u, tgBase = 0u, tg = 0u;
+        c.rays++;
+        for (;;) {
+            while (tg) {
+                const uint32_t k = tgBase + (uint32_t)__builtin_ctz(tg);
+                tg &= tg - 1u;
+                const float4* w = S.wprims + 3 * (size_t)k;
+                const Prim q{w[0], w[1], w[2]};
+                if (__float_as_uint(q.p2.w) != 0u) c.spheres++;
+                else c.tris++;
+                wideTest(q, o, d, inv, tmin, closest, best, bestLo, S.nprims > 1, redo);
+            }
+            if ((ng & 0xffu) == 0u) {
+                if (sp == 0) break;
+                sp--;
+                ng = my[sp * kWave];
+            }
+            const uint32_t bit = (uint32_t)__builtin_ctz(ng & 0xffu);
+            const uint32_t child = (ng >> 8) + (bit ^ oct);
+            ng &= ~(1u << bit);
+            if (ng & 0xffu) {
+                if (sp >= STACK) { atomicOr(S.err, 2u); break; }
+                my[sp * kWave] = ng;
+                sp++;
+            }
+            c.visits++;
+            const uint32_t off = child * 80u;
+            const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+            const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+            const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+            const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+            const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+            const uint32_t h = wideHits(n0, n1, n2, n3, n4, o, inv, oct, tmin, closest);
+            ng = (n1.x << 8) | (h >> 24);
+            tgBase = n1.y;
+            tg = h & 0xffffffu;
+        }
+        if (redo) {   // an order-dependent candidate: the query in the reference's order
+            closest = tmax;
+            const int k = traceRefStackless(S, o, d, tmin, closest);
+            best = k >= 0 ? (int)S.rankOf[k] : -1;
+        }
+        pt_hit hr = {};
+        hr.obj = -1;
+        hr.mat = -1;
+        if (best >= 0) {
+            HitRec x = makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d);
+            hr.hit = 1;
+            hr.obj = x.obj;
+            hr.mat = x.mat;
+            hr.front_face = x.front ? 1 : 0;
+            hr.t = closest;
+            hr.p[0] = x.p.x; hr.p[1] = x.p.y; hr.p[2] = x.p.z;
+            hr.n[0] = x.n.x; hr.n[1] = x.n.y; hr.n[2] = x.n.z;
+        }
+        hits[i] = hr;
     }
     waveReduceAdd(counters + 0, c.rays);
     waveReduceAdd(counters + 1, c.visits);
@@ -1739,9 +1940,10 @@ struct pt_scene {
     // build scratch, kept between builds: codes / ids (unsorted, sorted), scene box, sphere
     // flags, refit arrival counters, depth, sort temporary
     DevBuf codes, ids, codes2, ids2, box6, sph, arr, dep, sortTemp;
-    DevBuf wide;                            // 4-wide collapse of the LBVH (renderKernelWF<.., WIDE>), built on first use
+    DevBuf wide, wprims, wshade, rankOf;    // compressed 8-wide tree, its primitive and shading records, leaf ranks (PT_KERNEL_WIDE), built on first use
     int wideDepth = 0;
-    int64_t wideNodes = 0;
+    int64_t wideNodes = 0;                  // node slots
+    double wideBuildMs = 0.0;               // host build + upload, wall time
     int depth = 0;
     bool built = false;
     size_t deviceBytes = 0;
@@ -1770,92 +1972,42 @@ struct pt_film {
 };
 
 namespace {
-// Collapse the binary LBVH (device records downloaded into `bin`) into 4-wide nodes whose
-// entries follow the reference's DFS order (renderKernelWF<.., WIDE>).
-int buildWide4(pt_scene* s, const std::vector<float4>& bin) {
-    auto refOf = [&](int n, int slot) {
-        float f = slot == 0 ? bin[4 * (size_t)n + 3].x : bin[4 * (size_t)n + 3].y;
-        uint32_t r;
-        std::memcpy(&r, &f, 4);
-        return r;
-    };
-    auto boxOf = [&](int n, int slot, float b[6]) {
-        const float* f = reinterpret_cast<const float*>(&bin[4 * (size_t)n]);
-        for (int i = 0; i < 6; i++) b[i] = f[nodeBoxIdx(slot, i % 3, i / 3)];
-    };
-    struct Entry { uint32_t ref; bool internal; float box[6]; };
-    std::vector<float> out;   // 32 floats per wide node
-    std::vector<std::pair<int, int>> work{{0, 0}};   // (binary node, wide index)
-    std::vector<int> depth{1};
-    std::vector<int> nent{0};                           // entries per wide node
-    std::vector<std::vector<int>> kids(1);              // internal children per wide node
-    out.resize(32);
-    int maxDepth = 1;
-    for (size_t qi = 0; qi < work.size(); qi++) {
-        const int n = work[qi].first, w = work[qi].second;
-        std::vector<Entry> e;
-        auto add = [&](int parent, int slot) {
-            Entry x;
-            x.ref = refOf(parent, slot);
-            x.internal = !(x.ref & kLeafBit);
-            boxOf(parent, slot, x.box);
-            e.push_back(x);
-        };
-        auto expand = [&](int x) {   // [XL if leaf][XR if leaf][XR if internal][XL if internal]
-            const uint32_t xl = refOf(x, 0), xr = refOf(x, 1);
-            if (xl & kLeafBit) add(x, 0);
-            if (xr & kLeafBit) add(x, 1);
-            if (!(xr & kLeafBit)) add(x, 1);
-            if (!(xl & kLeafBit)) add(x, 0);
-        };
-        const uint32_t l = refOf(n, 0), r = refOf(n, 1);
-        if (l & kLeafBit) add(n, 0);
-        if (r & kLeafBit) add(n, 1);
-        if (!(r & kLeafBit)) expand((int)r);
-        if (!(l & kLeafBit)) expand((int)l);
-        float* W = &out[32 * (size_t)w];
-        for (int k = 0; k < 4; k++) {
-            const float inf = std::numeric_limits<float>::infinity();
-            float b[6] = {inf, inf, inf, -inf, -inf, -inf};
-            uint32_t ref = 0;
-            if (k < (int)e.size()) {
-                for (int i = 0; i < 6; i++) b[i] = e[k].box[i];
-                ref = e[k].ref;
-                if (e[k].internal) {
-                    const int wi = (int)(out.size() / 32);
-                    out.resize(out.size() + 32);
-                    W = &out[32 * (size_t)w];
-                    work.push_back({(int)e[k].ref, wi});
-                    depth.push_back(depth[qi] + 1);
-                    nent.push_back(0);
-                    kids.emplace_back();
-                    kids[w].push_back(wi);
-                    maxDepth = std::max(maxDepth, depth[qi] + 1);
-                    ref = (uint32_t)wi;
-                }
-            }
-            for (int a = 0; a < 6; a++) W[4 * a + k] = b[a];   // SoA planes
-            std::memcpy(&W[24 + k], &ref, 4);
-        }
-        for (int k = 28; k < 32; k++) W[k] = 0.0f;
-        nent[w] = (int)e.size();
-    }
-    // Worst-case stack use of the wide traversal (every entry hit): a visit pushes at most
-    // entries-1 items, then one subtree below it is active.  Children have larger indices.
-    std::vector<int> need(nent.size(), 0);
-    for (size_t w = nent.size(); w-- > 0;) {
-        int sub = 0;
-        for (int c : kids[w]) sub = std::max(sub, need[c]);
-        need[w] = std::max(0, nent[w] - 1) + sub;
-    }
-    if (out.size() / 32 >= (1u << 27)) return fail(PT_ERR_STATE, "too many wide nodes");
+// Build the compressed 8-wide tree on the host from the device's leaf-order primitive records
+// and exact leaf boxes (host/pt_wide8.cpp) and upload it.
+int buildWide(pt_scene* s) {
+    const int64_t n = s->nobj;
+    std::vector<uint32_t> prims((size_t)n * pt::kW8PrimDwords), shade((size_t)n * 12);
+    std::vector<float> boxes((size_t)n * 6);
+    HIP_TRY(hipMemcpy(prims.data(), s->prims.p, prims.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(shade.data(), s->shade.p, shade.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(boxes.data(), s->leafBoxes.p, boxes.size() * 4, hipMemcpyDeviceToHost));
+    // the reference's leaf order over the binary LBVH (child refs are dwords 12, 13 of a node)
+    std::vector<uint32_t> refs((size_t)std::max<int64_t>(1, n - 1) * 16);
+    if (n > 1) HIP_TRY(hipMemcpy(refs.data(), s->nodes.p, (size_t)(n - 1) * 64, hipMemcpyDeviceToHost));
+    const std::vector<uint32_t> rank = pt::referenceRanks(refs.data() + 12, refs.data() + 13, 16, n);
+    std::vector<uint32_t> wshade(shade.size());
+    for (int64_t k = 0; k < n; k++) std::memcpy(&wshade[(size_t)rank[k] * 12], &shade[(size_t)k * 12], 48);
+    pt::Wide8 w;
+    std::string err;
+    if (!pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, w, err)) return fail(PT_ERR_STATE, err);
     int rc;
-    if ((rc = devAlloc(s->wide, out.size() * 4))) return rc;
-    HIP_TRY(hipMemcpy(s->wide.p, out.data(), out.size() * 4, hipMemcpyHostToDevice));
-    s->wideDepth = need[0] + 1;   // stack entries needed (template choice); depth kept for info
-    (void)maxDepth;
-    s->wideNodes = (int64_t)(out.size() / 32);
+    if ((rc = devAlloc(s->wide, w.nodes.size() * 4)) || (rc = devAlloc(s->wprims, w.prims.size() * 4)) ||
+        (rc = devAlloc(s->wshade, wshade.size() * 4)) || (rc = devAlloc(s->rankOf, rank.size() * 4)))
+        return rc;
+    HIP_TRY(hipMemcpy(s->wide.p, w.nodes.data(), w.nodes.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->wprims.p, w.prims.data(), w.prims.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->wshade.p, wshade.data(), wshade.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->rankOf.p, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
+    s->wideDepth = w.depth;
+    s->wideNodes = (int64_t)(w.nodes.size() / pt::kW8NodeDwords);
     return PT_OK;
+}
+
+// Traversal stack entries of the wide kernels (one dword per entry): >= the tree depth.
+int wideStackFor(int depth) {
+    for (int st : {8, 16, 24})
+        if (depth <= st) return st;
+    return -1;
 }
 
 int setDevice(int dev) {
@@ -1868,37 +2020,57 @@ int setDevice(int dev) {
 }
 
 template <int S>
+void launchRenderWide(const RenderParams& P, hipStream_t st) {
+    if (P.partial) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
+    else renderKernelWF<S, false, true><<<P.ntiles, kWave, 0, st>>>(P);
+}
+template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
-    if (P.kernel == PT_KERNEL_WIDE && P.partial) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WIDE) renderKernelWF<S, false, true><<<P.ntiles, kWave, kCompatPad<S>, st>>>(P);
-    else if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
+    if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
         renderKernelWF<S, true, false><<<P.nwaves, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT)
-        renderKernelWF<S, false, false><<<P.ntiles, kWave, kCompatPad<S>, st>>>(P);
+        renderKernelWF<S, false, false><<<P.ntiles, kWave, 0, st>>>(P);
     else if (P.partial) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
-template <int S>
-int wavesPerCU(int kernel, int& n) {
-    const void* fn = kernel == PT_KERNEL_WIDE ? reinterpret_cast<const void*>(&renderKernelWF<S, true, true>)
-                                              : reinterpret_cast<const void*>(&renderKernelWF<S, true, false>);
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kWave, 0));
+template <int S, bool WIDE>
+int wavesPerCU(int& n) {
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&renderKernelWF<S, true, WIDE>),
+                                                         kWave, 0));
     return PT_OK;
 }
 int persistentWavesPerCU(int stack, int kernel, int& n) {
+    if (kernel == PT_KERNEL_WIDE) {
+        switch (stack) {
+            case 8: return wavesPerCU<8, true>(n);
+            case 16: return wavesPerCU<16, true>(n);
+            case 24: return wavesPerCU<24, true>(n);
+            default: return fail(PT_ERR_STATE, "unsupported wide BVH depth");
+        }
+    }
     switch (stack) {
-        case 16: return wavesPerCU<16>(kernel, n);
+        case 16: return wavesPerCU<16, false>(n);
 #if PT_STACK24
-        case 24: return wavesPerCU<24>(kernel, n);
+        case 24: return wavesPerCU<24, false>(n);
 #endif
-        case 32: return wavesPerCU<32>(kernel, n);
-        case 48: return wavesPerCU<48>(kernel, n);
-        case 64: return wavesPerCU<64>(kernel, n);
-        case 80: return wavesPerCU<80>(kernel, n);
+        case 32: return wavesPerCU<32, false>(n);
+        case 48: return wavesPerCU<48, false>(n);
+        case 64: return wavesPerCU<64, false>(n);
+        case 80: return wavesPerCU<80, false>(n);
         default: return fail(PT_ERR_STATE, "unsupported BVH depth");
     }
 }
 int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
+    if (P.kernel == PT_KERNEL_WIDE) {
+        switch (stack) {
+            case 8: launchRenderWide<8>(P, st); break;
+            case 16: launchRenderWide<16>(P, st); break;
+            case 24: launchRenderWide<24>(P, st); break;
+            default: return fail(PT_ERR_STATE, "unsupported wide BVH depth");
+        }
+        HIP_TRY(hipGetLastError());
+        return PT_OK;
+    }
     switch (stack) {
         case 16: launchRender<16>(P, st); break;
 #if PT_STACK24
@@ -1913,9 +2085,19 @@ int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
     HIP_TRY(hipGetLastError());
     return PT_OK;
 }
-int dispatchTrace(int stack, const DevScene& S, const pt_ray* r, int64_t n, float tmin, float tmax, pt_hit* h,
-                  unsigned long long* cnt, hipStream_t st) {
+int dispatchTrace(int stack, bool wide, const DevScene& S, const pt_ray* r, int64_t n, float tmin, float tmax,
+                  pt_hit* h, unsigned long long* cnt, hipStream_t st) {
     const unsigned blocks = (unsigned)((n + kWave - 1) / kWave);
+    if (wide) {
+        switch (stack) {
+            case 8: traceKernelWide<8><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 16: traceKernelWide<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 24: traceKernelWide<24><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            default: return fail(PT_ERR_STATE, "unsupported wide BVH depth");
+        }
+        HIP_TRY(hipGetLastError());
+        return PT_OK;
+    }
     switch (stack) {
         case 16: traceKernel<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
 #if PT_STACK24
@@ -1950,22 +2132,29 @@ DevScene devScene(const pt_scene* s) {
     S.shade = s->shade.as<float4>();
     S.mats = s->mats.as<float4>();
     S.wnodes = s->wide.as<float4>();
+    S.wprims = s->wprims.as<float4>();
+    S.wshade = s->wshade.as<float4>();
+    S.rankOf = s->rankOf.as<uint32_t>();
+    S.iparent = s->iparent.as<int>();
     S.err = reinterpret_cast<unsigned int*>(s->counters.as<unsigned long long>() + 7);
     S.nprims = (int)s->nobj;
     return S;
 }
 
-void fillStats(pt_stats* st, const unsigned long long c[5], double ms) {
+// Algorithmic bytes: per binary node visit both child boxes + refs (56 B), per
+// wide node visit the 80-B compressed record (8 child boxes, refs, frame); 40 B per triangle
+// test, 20 B per sphere test.
+void fillStats(pt_stats* st, const unsigned long long c[5], double ms, bool wide = false) {
     if (!st) return;
     std::memset(st, 0, sizeof(*st));
     st->rays = c[0];
     st->node_visits = c[1];
-    st->box_tests = 2 * c[1];
+    st->box_tests = (wide ? 8 : 2) * c[1];
     st->tri_tests = c[2];
     st->sphere_tests = c[3];
     st->paths = c[4];
     st->kernel_ms = ms;
-    st->algo_bytes = 56ull * c[1] + 40ull * c[2] + 20ull * c[3];
+    st->algo_bytes = (wide ? 80ull : 56ull) * c[1] + 40ull * c[2] + 20ull * c[3];
 }
 }  // namespace
 
@@ -2040,6 +2229,9 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     const int64_t n = s->nobj;
     s->built = false;
     s->wide.reset();
+    s->wprims.reset();
+    s->wshade.reset();
+    s->rankOf.reset();
     s->wideNodes = 0;
     s->wideDepth = 0;
     // Everything on the device, on one stream: scene box -> Morton codes -> radix sort ->
@@ -2122,15 +2314,14 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     return PT_OK;
 }
 
-// The 4-wide collapse is only needed by PT_KERNEL_WIDE: built from the device LBVH on first use.
+// The wide tree is only needed by PT_KERNEL_WIDE: built on first use after each LBVH build.
 static int ensureWide(pt_scene* s) {
-    if (s->wide.p || s->nobj <= 1) return PT_OK;
-    const size_t ni = (size_t)(s->nobj - 1);
-    std::vector<float4> tmp(ni * 4);
-    HIP_TRY(hipMemcpy(tmp.data(), s->nodes.p, ni * 4 * sizeof(float4), hipMemcpyDeviceToHost));
-    int rc = buildWide4(s, tmp);
+    if (s->wide.p || s->nobj <= 0) return PT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = buildWide(s);
     if (rc) return rc;
-    if (stackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");
+    s->wideBuildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (wideStackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");
     return PT_OK;
 }
 
@@ -2203,11 +2394,21 @@ int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
 
 int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, float tmax, pt_hit* hits,
                      pt_stats* stats) {
+    return pt_trace_closest_ex(s, rays, n, tmin, tmax, PT_KERNEL_DEFAULT, hits, stats);
+}
+
+int pt_trace_closest_ex(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel, pt_hit* hits,
+                        pt_stats* stats) {
     if (!s || n < 0 || (n > 0 && (!rays || !hits))) return fail(PT_ERR_INVALID, "pt_trace_closest: bad argument");
+    if (kernel != PT_KERNEL_DEFAULT && kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT &&
+        kernel != PT_KERNEL_WIDE)
+        return fail(PT_ERR_INVALID, "pt_trace_closest_ex: unknown kernel");
     if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
     int rc = setDevice(s->device);
     if (rc) return rc;
-    const int stack = s->nobj > 1 ? stackFor(s->depth) : 16;
+    const bool wide = kernel == PT_KERNEL_WIDE;
+    if (wide && (rc = ensureWide(s))) return rc;
+    const int stack = wide ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
     DevBuf dr, dh;
     if ((rc = devAlloc(dr, n * sizeof(pt_ray))) || (rc = devAlloc(dh, n * sizeof(pt_hit)))) return rc;
     if (n > 0) HIP_TRY(hipMemcpy(dr.p, rays, n * sizeof(pt_ray), hipMemcpyHostToDevice));
@@ -2216,7 +2417,7 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, 0));
-    if (n > 0 && (rc = dispatchTrace(stack, devScene(s), dr.as<pt_ray>(), n, tmin, tmax, dh.as<pt_hit>(),
+    if (n > 0 && (rc = dispatchTrace(stack, wide, devScene(s), dr.as<pt_ray>(), n, tmin, tmax, dh.as<pt_hit>(),
                                      s->counters.as<unsigned long long>(), 0))) {
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
         return rc;
@@ -2231,7 +2432,7 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     unsigned long long c[kNumCounters] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     c[4] = 0;
-    fillStats(stats, c, ms);
+    fillStats(stats, c, ms, wide);
     if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
     return PT_OK;
 }
@@ -2398,7 +2599,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (kernel == PT_KERNEL_WIDE) {
         if ((rc = ensureWide(s))) return rc;
         P.S = devScene(s);   // now with the wide nodes
-        if (s->nobj > 1 && !P.S.wnodes) return fail(PT_ERR_STATE, "wide BVH missing");
+        if (s->nobj > 0 && (!P.S.wnodes || !P.S.wprims)) return fail(PT_ERR_STATE, "wide BVH missing");
     }
     P.kernel = kernel;
     P.nblocks = 0;
@@ -2423,7 +2624,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
                                                    : envInt("PT_SHADE_BATCH", sampleRng ? 32 : 12);
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
-    const int stack = s->nobj > 1 ? stackFor(kernel == PT_KERNEL_WIDE ? s->wideDepth : s->depth) : 16;
+    const int stack = kernel == PT_KERNEL_WIDE ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
     const size_t ntl = (size_t)std::max(1, P.ntiles);
     if (!f->tileCost.p) {
         if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4))) return rc;
@@ -2545,7 +2746,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * outBpp, hipMemcpyDeviceToHost));
     unsigned long long c[kNumCounters] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
-    fillStats(stats, c, ms);
+    fillStats(stats, c, ms, kernel == PT_KERNEL_WIDE);
     if (std::getenv("PT_ITER_STATS") && c[8] + c[9] + c[10] > 0)   // diagnostic: wavefront scheduler
         std::fprintf(stderr, "[pt] iterations node %llu leaf %llu shade %llu | lanes/iter node %.1f leaf %.1f "
                      "shade %.1f\n", c[8], c[9], c[10], (double)c[1] / std::max(1ull, c[8]),
@@ -2555,6 +2756,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                      "shade %.3f\n", (double)c[12] / std::max(1ull, c[8]), (double)c[13] / std::max(1ull, c[9]),
                      (double)c[14] / std::max(1ull, c[10]), (double)c[12] / (double)(c[12] + c[13] + c[14]),
                      (double)c[13] / (double)(c[12] + c[13] + c[14]), (double)c[14] / (double)(c[12] + c[13] + c[14]));
+    if (std::getenv("PT_ITER_STATS") && kernel == PT_KERNEL_WIDE)
+        std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps)\n", c[20]);
     if (std::getenv("PT_ITER_STATS") && c[14] > 0)
         std::fprintf(stderr, "[pt] SHADE cycles/iteration: shading %.0f tasks %.0f new-path %.0f ray-start %.0f\n",
                      (double)c[16] / std::max(1ull, c[10]), (double)c[17] / std::max(1ull, c[10]),

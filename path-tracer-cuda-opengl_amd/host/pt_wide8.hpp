@@ -1,0 +1,43 @@
+// pt_wide8.hpp — host build of the compressed 8-wide BVH traversed by the wide render kernel.
+//
+// The reference traverses its binary LBVH depth first (RenderManager::hitBvh,
+// utils/render_manager.h:86-135).  The wide tree is an acceleration structure of this build
+// only: a binned-SAH binary tree over the same primitive records, collapsed to 8 children per
+// node, child boxes quantised outward to 8 bits per plane.  It changes which nodes are visited
+// and in which order, never which primitive is the closest hit ("Wide tree").
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pt {
+
+constexpr int kW8NodeDwords = 20;   // 80-B node record (layout in pt_wide8.cpp)
+constexpr int kW8PrimDwords = 12;   // 48-B primitive record
+
+struct Wide8 {
+    std::vector<uint32_t> nodes;   // kW8NodeDwords per node slot; slot 0 = root
+    std::vector<uint32_t> prims;   // kW8PrimDwords per primitive, in traversal (leaf) order
+    int depth = 0;                 // wide levels, root = 1 (= traversal stack entries needed)
+    int64_t usedNodes = 0;         // slots holding a node (children blocks are 8 slots, sparse)
+    int64_t leaves = 0;
+};
+
+// prims: n leaf-order (Morton) primitive records of kW8PrimDwords dwords (the device `prims`
+// array: {v0, mat}{v1, objID}{v2, sphere flag} or {c, mat}{r, 0, 0, objID}{0, 0, 0, 1});
+// boxes: n x {min xyz, max xyz}; rank: per leaf k its position in the reference's traversal
+// order (referenceRanks).  The output records carry the rank in place of the material id
+// ({v0, rank}...): ties between equal hit distances are decided by it, and it indexes the wide
+// kernels' shading records.  Returns false with `err` set when the tree exceeds the encoding
+// limits.
+bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
+                std::string& err);
+
+// The order in which RenderManager::hitBvh (render_manager.h:105-133) would test the leaves of
+// the binary LBVH if every box passed: at a node, its leaf children (left, then right), then the
+// right subtree, then the left one (the left child is pushed first, so the right one is popped
+// first).  refs: per internal node its two child refs (bit 31 = leaf, low 30 bits = leaf k).
+// Returns rank[k].
+std::vector<uint32_t> referenceRanks(const uint32_t* leftRef, const uint32_t* rightRef, size_t stride, int64_t n);
+
+}  // namespace pt

@@ -77,7 +77,7 @@ EXPORTS = [
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
     "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
-    "pt_scene_update_objects",
+    "pt_scene_update_objects", "pt_trace_closest_ex",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -106,6 +106,7 @@ _sig = {
     "pt_scene_bvh_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "pt_scene_download_bvh": (C.c_int, [_P, _P]),
     "pt_trace_closest": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, _P, C.POINTER(Stats)]),
+    "pt_trace_closest_ex": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, C.c_int, _P, C.POINTER(Stats)]),
     "pt_film_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                  C.POINTER(C.c_void_p)]),
     "pt_film_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
@@ -271,12 +272,13 @@ class Scene:
         _check(lib.pt_scene_download_bvh(self.h, _ptr(out) if len(out) else None), "pt_scene_download_bvh")
         return out
 
-    def trace(self, rays: np.ndarray, tmin: float = 0.001, tmax: float = float("inf")):
+    def trace(self, rays: np.ndarray, tmin: float = 0.001, tmax: float = float("inf"), kernel: int = KERNEL_DEFAULT):
+        """Closest hits (pt_trace_closest_ex): kernel=KERNEL_WIDE traverses the 8-wide tree."""
         rays = np.ascontiguousarray(rays, RAY_DTYPE)
         hits = np.zeros(len(rays), HIT_DTYPE)
         st = Stats()
-        _check(lib.pt_trace_closest(self.h, _ptr(rays) if len(rays) else None, len(rays), tmin, tmax,
-                                    _ptr(hits) if len(hits) else None, C.byref(st)), "pt_trace_closest")
+        _check(lib.pt_trace_closest_ex(self.h, _ptr(rays) if len(rays) else None, len(rays), tmin, tmax, kernel,
+                                       _ptr(hits) if len(hits) else None, C.byref(st)), "pt_trace_closest_ex")
         return hits, st
 
     def close(self) -> None:

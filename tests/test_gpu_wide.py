@@ -1,0 +1,133 @@
+"""The compressed 8-wide tree (PT_KERNEL_WIDE) against the oracle's reference-order traversal.
+
+The wide tree visits nodes in its own order (nearest child first) through conservative,
+8-bit quantised boxes; the closest hit is the minimum of (t, the reference's tie order), which is
+the hit the reference's left-first DFS keeps.  The bar is therefore the same as for the binary
+kernels: every hit record bit-exact, including exact ties (duplicated triangles and spheres).
+"""
+import numpy as np
+import pytest
+
+from helpers import OBJECT_DTYPE, MATERIAL_DTYPE, deep_stack_scene, random_rays, random_soup, rays_to_struct
+
+pytestmark = pytest.mark.gpu
+
+SCENES = ["triangle_world", "random_world", "test_world", "rtiow", "cornell", "bunny_cornell"]
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def assert_hits_equal(g, o):
+    for f in ("hit", "obj", "mat", "front_face"):
+        np.testing.assert_array_equal(g[f], o[f], err_msg=f)
+    h = g["hit"] == 1
+    for f in ("t", "p", "n"):
+        np.testing.assert_array_equal(bits(g[f][h]), bits(o[f][h]), err_msg=f)
+
+
+def trace_both(pt, orc, gpu, objs, mats, rays, tmin=0.001, tmax=np.inf):
+    s = pt.Scene(objs, mats, device=gpu)
+    hits, st = s.trace(rays_to_struct(rays, pt.RAY_DTYPE), tmin, tmax, kernel=pt.KERNEL_WIDE)
+    ref, rst = orc.trace(objs, orc.build_lbvh(objs, orc.morton_keys(objs), tight=True), rays, tmin, tmax)
+    return hits, st, ref, rst
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_wide_trace_matches_oracle(pt, orc, gpu, name):
+    p = pt.Preset(name)
+    lo = p.objects["v"][:, :3].min(0)
+    hi = p.objects["v"][:, :3].max(0)
+    center = np.clip((lo + hi) / 2, -1e3, 1e3)
+    radius = float(min(np.linalg.norm(hi - lo), 3000.0)) * 0.75 + 1.0
+    rays = random_rays(8192, seed=2, center=center, radius=radius, objects=p.objects)
+    hits, st, ref, rst = trace_both(pt, orc, gpu, p.objects, p.materials, rays)
+    assert_hits_equal(hits, ref)
+    assert hits["hit"].sum() > 100
+    assert st.rays == len(rays)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_wide_trace_random_soup(pt, orc, gpu, seed):
+    objs, mats = random_soup(3000, 500, seed=seed)
+    rays = random_rays(8192, seed=seed + 10, objects=objs)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    assert_hits_equal(hits, ref)
+
+
+def test_wide_trace_tmin_tmax_window(pt, orc, gpu):
+    objs, mats = random_soup(500, 100, seed=3)
+    rays = random_rays(2048, seed=4, objects=objs)
+    for tmin, tmax in ((0.001, 5.0), (2.0, 40.0), (0.0, np.inf)):
+        hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays, tmin, tmax)
+        assert_hits_equal(hits, ref)
+
+
+def tie_scene(seed=5):
+    """Exact ties: every triangle three times and every sphere three times (identical geometry,
+    different materials), so the reference's order decides which copy is the hit: the FIRST
+    triangle in key order (a later t == closest is rejected), the LAST sphere (t <= closest)."""
+    objs, mats = random_soup(400, 120, seed=seed, n_mat=6)
+    rep = np.concatenate([objs, objs, objs])
+    rep["mat"][len(objs):2 * len(objs)] = (objs["mat"] + 1) % 6
+    rep["mat"][2 * len(objs):] = (objs["mat"] + 2) % 6
+    perm = np.random.default_rng(seed).permutation(len(rep))
+    return rep[perm], mats
+
+
+def test_wide_trace_exact_ties(pt, orc, gpu):
+    objs, mats = tie_scene()
+    rays = random_rays(8192, seed=6, objects=objs)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    assert_hits_equal(hits, ref)
+    # the ties matter: the copies differ in material, and many rays hit a duplicated object
+    assert (ref["hit"] == 1).sum() > 2000
+
+
+def test_wide_trace_coplanar_sphere_ties(pt, orc, gpu):
+    """Concentric spheres of equal radius (the deep-stack scene: 2,048 identical spheres)."""
+    objs, mats = deep_stack_scene(n_group=256)
+    objs["mat"] = np.arange(len(objs)) % 1
+    rays = random_rays(4096, seed=8, center=(1024.0, 1024.0, 1024.0), radius=3000.0, objects=objs)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    assert_hits_equal(hits, ref)
+
+
+def test_wide_trace_c5(pt, orc, gpu):
+    p = pt.Preset("bunny_field", 64, 36)
+    rays = random_rays(8192, seed=9, center=(278, 150, 280), radius=700, objects=p.objects)
+    hits, st, ref, rst = trace_both(pt, orc, gpu, p.objects, p.materials, rays)
+    assert_hits_equal(hits, ref)
+    assert st.node_visits < rst.node_visits   # the point of the wide tree
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 9])
+def test_wide_tiny_scenes(pt, orc, gpu, n):
+    """Roots that are a leaf (n <= 3) or a single wide node."""
+    objs, mats = random_soup(n - n // 2, n // 2, seed=n)
+    rays = random_rays(2048, seed=n, objects=objs)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    assert_hits_equal(hits, ref)
+
+
+def test_wide_render_ties_bit_exact(pt, orc, gpu):
+    """A rendered frame of the tie scene: every bounce's hit must be the reference's copy."""
+    objs, mats = tie_scene(seed=11)
+    w, h = 48, 32
+    cam = pt.camera_make((0.0, 0.0, 30.0), (0.0, 0.0, 0.0), 50.0, w / h)
+    s = pt.Scene(objs, mats, device=gpu)
+    f = pt.Film(w, h, 5, device=gpu)
+    nodes = orc.build_lbvh(objs, orc.morton_keys(objs), tight=True)
+    for rng in ("compat", "sample"):
+        f.reset()
+        if rng == "compat":
+            rgb, st = pt.render(s, f, cam, 3, 12, kernel=pt.KERNEL_WIDE)
+            ref, rst = orc.render(objs, mats, nodes, pt.camera_to_array(cam), w, h, f.rows, 3, 12,
+                                  orc.film_states(5, w, f.rows), nthreads=8)
+        else:
+            rgb, st = pt.render(s, f, cam, 3, 12, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE, chunk=2)
+            ref, rst = orc.render_sample(objs, mats, nodes, pt.camera_to_array(cam), w, h, f.rows, 3, 12, 5, 2,
+                                         nthreads=8)
+        np.testing.assert_array_equal(bits(rgb), bits(ref), err_msg=rng)
+        assert st.rays == rst.rays
