@@ -16,11 +16,17 @@ sequential chain, and the slowest pixels (paths trapped under the bunny, ~40 ray
 the frame at ~1.8 s however many GPUs share it.  At N = 1 the line also carries one compat frame
 (`compat_mode`).  Both modes render the same image in distribution (tests/test_oracle.py).
 
+Kernel (--kernel): `wide` (default) traverses the compressed 8-wide SAH tree nearest child
+first and keeps the reference's closest hit by (t, the reference's tie order); `wavefront` walks
+the binary LBVH in the reference's own order.  Both render the same image bit for bit.
+
 Rank 0 prints one JSON line.  `value` = total closest-hit queries (counted in-kernel, all
 ranks) / max-over-ranks wall time of the K timed frames.  `roofline.achieved` = algorithmic
-bytes (56 B per internal-node visit + 40 B per triangle test + 20 B per sphere
-test) / render-kernel time from HIP events on the render stream.  `cpu_baseline` = the CPU
-restatement (oracle/) on the host cores, rank 0 at N = 1 only, on a bounded sample.
+bytes of the traversed tree (per node visit its child boxes and refs -- 56 B
+binary, 80 B 8-wide compressed -- + 40 B per triangle test + 20 B per sphere test) / render-kernel
+time from HIP events on the render stream, against the L2 ceiling (the tree is L2-resident; the
+HBM fraction of the PMC traffic is reported beside it).  `cpu_baseline` = the CPU restatement
+(oracle/) on the host cores, rank 0 at N = 1 only, on a bounded sample.
 """
 import argparse
 import json
@@ -38,7 +44,9 @@ import ptamd  # noqa: E402
 import ptdist  # noqa: E402
 
 METRIC = "Mray/s + ms/frame, bunny-in-Cornell 1920×1080 @1024spp, 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md "HBM": HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md "L2 (per XCD)": 4 MiB per XCD, ~34.5 TB/s aggregate
+GATHER_CEILING_GBS = 16000.0   # tools/micro/chase.hip: dependent per-lane gathers of 64-B records, L2-resident
 CONFIGS = {
     "c3": ("bunny_cornell", "bunny-in-Cornell (5,000 tris) 1920x1080 @1024spp depth 50 (C3)"),
     "c2": ("cornell", "Cornell box (32 tris) 800x800 @256spp depth 8 (C2)"),
@@ -75,16 +83,17 @@ def cpu_baseline(preset, budget_s: float = 12.0) -> dict:
                       f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads"}
 
 
-def pmc_traffic(workload: str, spp: int, rng: str):
+def pmc_traffic(workload: str, spp: int, rng: str, kernel: str):
     """Per-launch HBM traffic of the render kernel on this exact workload, from the committed
     rocprofv3 PMC passes (profiles/traffic.json, written by tools/collect_profile.py); None if the
-    profile is for a different configuration."""
+    profile is for a different configuration or kernel."""
     path = os.path.join(REPO, "profiles", "traffic.json")
     try:
         t = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    if t.get("workload") != workload or t.get("spp") != spp or t.get("rng") != rng:
+    if (t.get("workload") != workload or t.get("spp") != spp or t.get("rng") != rng or
+            t.get("kernel", "wavefront") != kernel):
         return None, None
     return t["traffic_bytes_per_launch"], t["source"]
 
@@ -243,7 +252,9 @@ def main() -> None:
         rng_desc = (("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
                      f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
                     "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)")
-        traffic, traffic_src = pmc_traffic(workload, spp, rng_desc)
+        traffic, traffic_src = pmc_traffic(workload, spp, rng_desc, args.kernel)
+        kernel_s = kms / 1e3 / args.steps if kms > 0 else 0.0
+        hbm_gbs = traffic / kernel_s / 1e9 if (traffic and kernel_s > 0) else None
         out = {
             "metric": METRIC,
             "value": total_rays / elapsed / 1e6,
@@ -265,18 +276,27 @@ def main() -> None:
                        "rng": ("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
                                f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
                               "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            # The traversal's working set (tree + primitive + shading records: 0.5 MB for C3) is
+            # L2-resident: its bytes come from L2 and L1, HBM traffic is the per-task block sums
+            # (`hbm`, PMC).  The applicable memory ceiling is L2 bandwidth; the measured ceiling of
+            # this access pattern (dependent per-lane gathers) is `gather_ceiling`.
+            "roofline": {"bound": "l2", "achieved": achieved, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / L2_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "renderKernelWF", "kernel_ms_per_launch": kms / args.steps,
+                         "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
+                                 "frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs is not None else None},
+                         "gather_ceiling": {"peak": GATHER_CEILING_GBS, "frac": achieved / GATHER_CEILING_GBS,
+                                            "source": "tools/micro/chase.hip, DESIGN.md section 6"},
+                         "kernel": "renderKernelWF<STACK, SAMPLE, WIDE=%s>" % ("true" if args.kernel == "wide" else "false"),
+                         "kernel_ms_per_launch": kms / args.steps,
                          "algo_bytes_per_launch": kbytes / args.steps,
-                         "algo_bytes_source": "reference-order traversal counts of the same frame "
-                                              "(ray-synchronous kernel, warmup step 1)",
-                         "note": "algorithmic bytes (SURVEY 8(d): 56 B/node visit + 40 B/triangle test) consumed "
-                                 "per kernel second; the BVH is cache-resident (L2 for C2/C3), so frac can "
-                                 "exceed 1 -- HBM bytes actually moved per launch are `traffic` (PMC)",
+                         "algo_bytes_source": ("the wide kernel's own counts: 80 B per 8-wide node visit + 40 B per "
+                                               "triangle test + 20 B per sphere test" if args.kernel == "wide" else
+                                               "reference-order traversal counts of the same frame (ray-synchronous "
+                                               "kernel, warmup step 1): 56 B per binary node visit + 40 B per "
+                                               "triangle test + 20 B per sphere test"),
                          "node_visits_reference": ref_st.node_visits,
-                         "node_visits_wavefront": spec_visits / args.steps},
+                         "node_visits_kernel": spec_visits / args.steps},
         }
         if compat:
             out["compat_mode"] = compat

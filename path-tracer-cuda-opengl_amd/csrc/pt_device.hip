@@ -2588,7 +2588,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (kernel == PT_KERNEL_DEFAULT) {
         const char* k = std::getenv("PT_RENDER_KERNEL");
         const std::string ks = k ? k : "";
-        kernel = ks == "simple" ? PT_KERNEL_SIMPLE : (ks == "wide" ? PT_KERNEL_WIDE : PT_KERNEL_WAVEFRONT);
+        kernel = ks == "simple" ? PT_KERNEL_SIMPLE : (ks == "wavefront" ? PT_KERNEL_WAVEFRONT : PT_KERNEL_WIDE);
     }
     if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
         return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -55,11 +56,26 @@ struct BNode {
     int32_t first = 0, count = 0;    // leaf: idx[first, first + count)
 };
 
-constexpr int kMaxLeaf = 3;
 constexpr int kBins = 32;
-constexpr double kTravCost = 1.0, kPrimCost = 1.0;   // SAH weights (node visit vs primitive test)
+constexpr double kPrimCost = 1.0;
+
+// Build parameters (tuning knobs, PT_WIDE_MAX_LEAF / PT_WIDE_TRAV_COST): at most kMaxLeaf <= 3
+// primitives per leaf (the meta byte's unary count); the SAH weight of a binary node visit
+// relative to a primitive test.
+int envLeaf() {
+    const char* v = std::getenv("PT_WIDE_MAX_LEAF");
+    const int x = v ? std::atoi(v) : 0;
+    return x >= 1 && x <= 3 ? x : 3;
+}
+double envTrav() {
+    const char* v = std::getenv("PT_WIDE_TRAV_COST");
+    const double x = v ? std::atof(v) : 0.0;
+    return x > 0.0 ? x : 1.0;
+}
 
 struct SahBuilder {
+    int kMaxLeaf = 3;
+    double kTravCost = 1.0;
     const BBox* boxes = nullptr;
     std::vector<float> cen;           // centroids, 3 per primitive
     std::vector<int32_t> idx;
@@ -213,6 +229,8 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
         return false;
     }
     SahBuilder B;
+    B.kMaxLeaf = envLeaf();
+    B.kTravCost = envTrav();
     B.boxes = reinterpret_cast<const BBox*>(boxes);
     B.cen.resize((size_t)n * 3);
     B.idx.resize((size_t)n);

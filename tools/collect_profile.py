@@ -47,6 +47,7 @@ def main(tag):
     cfg = bench["config"]
     out = {
         "workload": cfg["workload"], "spp": cfg["spp"], "rng": cfg["rng"],
+        "kernel": "wide" if "WIDE=true" in bench["roofline"].get("kernel", "") else "wavefront",
         "traffic_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes": fetch_b, "write_bytes": write_b,
         "source": f"profiles/{tag}/pmc_fetch.csv + pmc_write.csv (separate rocprofv3 --pmc passes; "
