@@ -332,18 +332,14 @@ __device__ __forceinline__ SlabHit refLeafBox(const Prim& q, bool sphere, float3
         const float r = fabsf(q.p1.x);
         mn[0] = q.p0.x - r; mn[1] = q.p0.y - r; mn[2] = q.p0.z - r;
         mx[0] = q.p0.x + r; mx[1] = q.p0.y + r; mx[2] = q.p0.z + r;
-    } else {
-        mn[0] = mx[0] = q.p0.x; mn[1] = mx[1] = q.p0.y; mn[2] = mx[2] = q.p0.z;
-        const float4 v[2] = {q.p1, q.p2};
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            if (mn[0] > v[i].x) mn[0] = v[i].x;
-            if (mn[1] > v[i].y) mn[1] = v[i].y;
-            if (mn[2] > v[i].z) mn[2] = v[i].z;
-            if (mx[0] < v[i].x) mx[0] = v[i].x;
-            if (mx[1] < v[i].y) mx[1] = v[i].y;
-            if (mx[2] < v[i].z) mx[2] = v[i].z;
-        }
+    } else {   // utils::unionPoints (aabb.h:68-79); vertices are never NaN, so v_min3 / v_max3
+        // give the same planes (up to the sign of a zero, which no slab comparison sees)
+        mn[0] = fminf(fminf(q.p0.x, q.p1.x), q.p2.x);
+        mn[1] = fminf(fminf(q.p0.y, q.p1.y), q.p2.y);
+        mn[2] = fminf(fminf(q.p0.z, q.p1.z), q.p2.z);
+        mx[0] = fmaxf(fmaxf(q.p0.x, q.p1.x), q.p2.x);
+        mx[1] = fmaxf(fmaxf(q.p0.y, q.p1.y), q.p2.y);
+        mx[2] = fmaxf(fmaxf(q.p0.z, q.p1.z), q.p2.z);
     }
     return slabPair(v2f{mn[0], mx[0]}, v2f{mn[1], mx[1]}, v2f{mn[2], mx[2]}, o, inv, tmin, tmax);
 }
@@ -1222,11 +1218,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (h0) { k0 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
                 const bool h1 = tg != 0u;
                 if (h1) { k1 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
-                const float4* w0 = S.wprims + 3 * (size_t)k0;
-                const float4* w1 = S.wprims + 3 * (size_t)k1;
                 Prim q0{}, q1{};
-                if (h0) q0 = Prim{w0[0], w0[1], w0[2]};
-                if (h1) q1 = Prim{w1[0], w1[1], w1[2]};
+                {
+                    const float4* w0 = S.wprims + 3 * (size_t)k0;
+                    const float4* w1 = S.wprims + 3 * (size_t)k1;
+                    if (h0) q0 = Prim{w0[0], w0[1], w0[2]};
+                    if (h1) q1 = Prim{w1[0], w1[1], w1[2]};
+                }
                 bool redo = false;
                 if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                 if (h1) wideTest(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
