@@ -856,6 +856,10 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
+#ifndef PT_WIDE_PARK
+#define PT_WIDE_PARK 1   // wide kernels keep the path state in LDS between SHADE steps
+#endif
+constexpr int kParkWords = 18;
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
@@ -877,6 +881,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // per SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
     constexpr int LS = kLdsStack<STACK, SAMPLE, WIDE>;
     __shared__ uint32_t stk[LS * kWave];
+    // Wide kernels park the lane's path state (RNG, attenuation, sums, sample bookkeeping: only
+    // SHADE steps use them) in LDS between SHADE steps, so NODE / LEAF steps run with the ray and
+    // traversal state alone in registers (6 waves per SIMD without spills).  park[w * 64 + lane].
+    constexpr bool PARK = WIDE && PT_WIDE_PARK;
+    __shared__ uint32_t park[PARK ? kParkWords * kWave : 1];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -914,9 +923,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #endif
 
     Xorwow g{};
-    uint32_t cr = 0;     // sample mode: the task's pixel, col | local row << 16
+    uint32_t cr = 0;     // sample mode: the task's pixel, col | local row << 16 (parking wide kernels: compat too)
     if constexpr (!SAMPLE) {
         if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
+        if constexpr (PARK) cr = (uint32_t)col | ((uint32_t)lrow << 16);
     }
     float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
@@ -1040,6 +1050,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
+        if constexpr (PARK && !SAMPLE) fcol = (float)(cr & 0xffffu);                              \
         if constexpr (SAMPLE) {                                                                   \
             fcol = (float)(cr & 0xffffu);                                                         \
             g = sampleStream(P.seed0, P.seed1, P.sampleBase + (uint32_t)sample,                   \
@@ -1090,6 +1101,36 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     sRays += (uint32_t)__popcll(__ballot(started));
     sPaths += (uint32_t)__popcll(__ballot(started)) +
               (!SAMPLE && P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
+#define PT_PARK()                                                                                   \
+    do {                                                                                          \
+        if constexpr (PARK) {                                                                     \
+            uint32_t* pk_ = park + lane;                                                          \
+            pk_[0 * kWave] = g.d; pk_[1 * kWave] = g.v0; pk_[2 * kWave] = g.v1;                   \
+            pk_[3 * kWave] = g.v2; pk_[4 * kWave] = g.v3; pk_[5 * kWave] = g.v4;                  \
+            pk_[6 * kWave] = __float_as_uint(att.x); pk_[7 * kWave] = __float_as_uint(att.y);     \
+            pk_[8 * kWave] = __float_as_uint(att.z); pk_[9 * kWave] = __float_as_uint(sum.x);     \
+            pk_[10 * kWave] = __float_as_uint(sum.y); pk_[11 * kWave] = __float_as_uint(sum.z);   \
+            pk_[12 * kWave] = (uint32_t)depthLeft; pk_[13 * kWave] = (uint32_t)sample;            \
+            pk_[14 * kWave] = (uint32_t)nSamples; pk_[15 * kWave] = cr;                           \
+            pk_[16 * kWave] = __float_as_uint(frow); pk_[17 * kWave] = taskRays;                  \
+        }                                                                                         \
+    } while (0)
+#define PT_UNPARK()                                                                                 \
+    do {                                                                                          \
+        if constexpr (PARK) {                                                                     \
+            const uint32_t* pk_ = park + lane;                                                    \
+            g = Xorwow{pk_[0 * kWave], pk_[1 * kWave], pk_[2 * kWave], pk_[3 * kWave], pk_[4 * kWave], \
+                       pk_[5 * kWave]};                                                           \
+            att = f3(__uint_as_float(pk_[6 * kWave]), __uint_as_float(pk_[7 * kWave]),             \
+                     __uint_as_float(pk_[8 * kWave]));                                            \
+            sum = f3(__uint_as_float(pk_[9 * kWave]), __uint_as_float(pk_[10 * kWave]),            \
+                     __uint_as_float(pk_[11 * kWave]));                                           \
+            depthLeft = (int)pk_[12 * kWave]; sample = (int)pk_[13 * kWave];                      \
+            nSamples = (int)pk_[14 * kWave]; cr = pk_[15 * kWave];                                \
+            frow = __uint_as_float(pk_[16 * kWave]); taskRays = pk_[17 * kWave];                  \
+        }                                                                                         \
+    } while (0)
+    PT_PARK();
 
     for (;;) {
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
@@ -1280,19 +1321,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }
         if (kind == 2) {
             // ------------------------------------------------------------------ SHADE
+            if constexpr (WIDE) {
+                // rare: an order-dependent query, repeated in the reference's order (before the
+                // path state comes back from LDS: only the ray is live here).  Ranks index wshade.
+                const bool redo = wantShade && !needTask && (oct & 8u);
+                PT_DIAG_ADD(sRedo, (uint32_t)__popcll(__ballot(redo)));
+                if (redo) {
+                    closest = __builtin_inff();
+                    const int k = traceRefStackless(S, o, d, 0.001f, closest);
+                    best = k >= 0 ? (int)S.rankOf[k] : -1;
+                }
+            }
+            PT_UNPARK();
             bool newRay = false, newSample = false;
             PT_DIAG_ADD(itS, 1u);
-            if constexpr (WIDE) PT_DIAG_ADD(sRedo, (uint32_t)__popcll(__ballot(wantShade && !needTask && (oct & 8u))));
             if (wantShade && !needTask) {
                 bool done = false;
                 float3 contrib = f3(0.0f, 0.0f, 0.0f);
-                if constexpr (WIDE) {
-                    if (oct & 8u) {   // rare: the query in the reference's order (ranks index wshade)
-                        closest = __builtin_inff();
-                        const int k = traceRefStackless(S, o, d, 0.001f, closest);
-                        best = k >= 0 ? (int)S.rankOf[k] : -1;
-                    }
-                }
                 if (best < 0) {
                     contrib = sky(d, att);
                     done = true;
@@ -1346,6 +1391,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #endif
             sRays += (uint32_t)__popcll(__ballot(newRay));
             sPaths += (uint32_t)__popcll(__ballot(newSample));
+            PT_PARK();
         }
 #ifdef PT_DIAG
         {   // shader-clock cycles per step kind (the step's memory waits included)
@@ -1356,7 +1402,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }
 #endif
     }
+    PT_UNPARK();
     if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
+        if constexpr (PARK) idx = (cr >> 16) * (uint32_t)P.width + (cr & 0xffffu);
         if (valid) {
             storePixel(P, idx, sum);
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
@@ -1397,6 +1445,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     }
 }
 #undef PT_BEGIN_RAY
+#undef PT_PARK
+#undef PT_UNPARK
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK

@@ -252,6 +252,8 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
     int emin = ext > 0.0 ? (int)std::ceil(std::log2(ext)) - 20 : -100;
     emin = std::max(emin, -100);
 
+    const char* sl = std::getenv("PT_WIDE_SPLIT_LEAVES");
+    const bool splitLeaves = !(sl && *sl == '0');
     struct Work { int32_t bnode; int64_t slot; int depth; };
     std::vector<Work> work{{root, 0, 1}};
     out.nodes.assign(kW8NodeDwords, 0u);
@@ -261,7 +263,7 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
         out.depth = std::max(out.depth, w.depth);
         // children: open the largest internal child until 8 (a leaf root is its own single child)
         std::vector<int32_t> ch;
-        const BNode& bn = B.nodes[w.bnode];
+        const BNode bn = B.nodes[w.bnode];
         if (bn.count > 0) ch.push_back(w.bnode);
         else ch = {bn.left, bn.right};
         while (ch.size() < 8) {
@@ -279,6 +281,29 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
             const int32_t l = c.left, r = c.right;
             ch[bi] = l;
             ch.insert(ch.begin() + bi + 1, r);
+        }
+        // free slots left (every internal child opened): split multi-primitive leaves, largest
+        // first, so more primitives get a box of their own (the slots are tested anyway)
+        while (splitLeaves && ch.size() < 8) {
+            int bi = -1;
+            for (int i = 0; i < (int)ch.size(); i++) {
+                const BNode& c = B.nodes[ch[i]];
+                if (c.count > 1 && (bi < 0 || c.count > B.nodes[ch[bi]].count)) bi = i;
+            }
+            if (bi < 0) break;
+            const BNode c = B.nodes[ch[bi]];
+            BNode a, b;
+            a.first = c.first;
+            a.count = 1;
+            b.first = c.first + 1;
+            b.count = c.count - 1;
+            a.box = B.boxes[B.idx[c.first]];
+            b.box = emptyBox();
+            for (int32_t i = b.first; i < b.first + b.count; i++) growBox(b.box, B.boxes[B.idx[i]]);
+            B.nodes.push_back(a);
+            ch[bi] = (int32_t)B.nodes.size() - 1;
+            B.nodes.push_back(b);
+            ch.insert(ch.begin() + bi + 1, (int32_t)B.nodes.size() - 1);
         }
         BBox nb = emptyBox();
         for (int32_t c : ch) growBox(nb, B.nodes[c].box);
