@@ -857,7 +857,8 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
 #ifndef PT_WIDE_PARK
-#define PT_WIDE_PARK 1   // wide kernels keep the path state in LDS between SHADE steps
+#define PT_WIDE_PARK 0   // 1: wide kernels keep the path state in LDS between SHADE steps (80 VGPRs fit at 6 waves;
+                         // C3 @256 spp: 5 waves 172.4 ms, 6 waves 174.6 ms, not parked at 5 waves 166.8 ms)
 #endif
 constexpr int kParkWords = 18;
 #ifndef PT_WIDE_WAVES_PER_EU
