@@ -131,3 +131,34 @@ def test_wide_render_ties_bit_exact(pt, orc, gpu):
                                          nthreads=8)
         np.testing.assert_array_equal(bits(rgb), bits(ref), err_msg=rng)
         assert st.rays == rst.rays
+
+
+@pytest.mark.parametrize("cfg,w,h,spp", [("bunny_cornell", 240, 135, 4), ("bunny_field", 160, 90, 2), ("cornell", 128, 128, 8)])
+def test_wide_frame_equals_reference_order_frame(pt, gpu, cfg, w, h, spp):
+    """Whole frames (both RNG modes) from the wide kernel equal the binary kernel's, which follows
+    the reference's own visiting order (itself bit-exact against the oracle, test_gpu_parity.py)."""
+    p = pt.Preset(cfg, w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    for rng in (pt.RNG_COMPAT, pt.RNG_SAMPLE):
+        out = {}
+        for k in (pt.KERNEL_WAVEFRONT, pt.KERNEL_WIDE):
+            f = pt.Film(w, h, 7, device=gpu)
+            out[k] = pt.render(s, f, p.camera, spp, p.max_depth, kernel=k, rng=rng)
+        np.testing.assert_array_equal(bits(out[pt.KERNEL_WIDE][0]), bits(out[pt.KERNEL_WAVEFRONT][0]))
+        assert out[pt.KERNEL_WIDE][1].rays == out[pt.KERNEL_WAVEFRONT][1].rays
+
+
+def test_wide_large_soup_trace_and_render(pt, orc, gpu):
+    """200,000 random triangles and spheres: hit records against the oracle, and a frame against
+    the reference-order kernel."""
+    objs, mats = random_soup(150_000, 50_000, seed=12, spread=60.0)
+    rays = random_rays(8192, seed=13, radius=90.0, objects=objs)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    assert_hits_equal(hits, ref)
+    s = pt.Scene(objs, mats, device=gpu)
+    cam = pt.camera_make((0.0, 20.0, 120.0), (0.0, 0.0, 0.0), 45.0, 1.5)
+    frames = []
+    for k in (pt.KERNEL_WAVEFRONT, pt.KERNEL_WIDE):
+        f = pt.Film(96, 64, 3, device=gpu)
+        frames.append(pt.render(s, f, cam, 2, 12, kernel=k, rng=pt.RNG_SAMPLE, chunk=2)[0])
+    np.testing.assert_array_equal(bits(frames[1]), bits(frames[0]))
