@@ -30,6 +30,7 @@
 #include "../host/pt_error.hpp"
 #include "../host/pt_host.hpp"
 #include "../host/pt_wide8.hpp"
+#include "../host/pt_wide_dev.hpp"
 #include "pt.h"
 
 using pt::fail;
@@ -1673,7 +1674,7 @@ __device__ __forceinline__ int deltaK(const unsigned long long* k, long long n, 
 // generateLBVH (bvh.h:71-115) with the node reset separated from the linking (no race):
 // writes child refs of internal node i and the parent link of both children.
 __global__ void karrasKernel(const unsigned long long* __restrict__ keys, int n, float4* nodes, int* iparent,
-                             int* lparent, const uint32_t* __restrict__ leafSphere) {
+                             int* lparent, const uint32_t* __restrict__ leafSphere, int2* irange) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n - 1) return;
     // determineRange (bvh.h:17-40)
@@ -1708,6 +1709,7 @@ __global__ void karrasKernel(const unsigned long long* __restrict__ keys, int n,
     if (split + 1 == last) { b = kLeafBit | (leafSphere[split + 1] ? kSphereBit : 0u) | (uint32_t)(split + 1); lparent[split + 1] = i; }
     else { b = (uint32_t)(split + 1); iparent[split + 1] = i; }
     nodes[4 * (size_t)i + 3] = make_float4(__uint_as_float(a), __uint_as_float(b), 0.0f, 0.0f);
+    irange[i] = make_int2(first, last);   // leaf range (the device wide build's ranks)
 }
 
 // Writes a child box into slot (0 = left, 1 = right) of node p with write-through stores.
@@ -1989,7 +1991,11 @@ struct pt_scene {
     // build scratch, kept between builds: codes / ids (unsorted, sorted), scene box, sphere
     // flags, refit arrival counters, depth, sort temporary
     DevBuf codes, ids, codes2, ids2, box6, sph, arr, dep, sortTemp;
-    DevBuf wide, wprims, wshade, rankOf;    // compressed 8-wide tree, its primitive and shading records, leaf ranks (PT_KERNEL_WIDE), built on first use
+    DevBuf irange;                          // leaf range [first, last] per internal node
+    DevBuf wide, wprims, wshade, rankOf;    // compressed 8-wide tree, its primitive and shading records, leaf ranks (PT_KERNEL_WIDE)
+    std::unique_ptr<pt::WideDevBuilder> wideDev;   // device build scratch (PT_BVH_WIDE_DEVICE), kept between builds
+    bool wideReady = false;                 // the wide tree matches the current LBVH build
+    int wideSource = 0;                     // 1: host binned SAH, 2: device PLOC
     int wideDepth = 0;
     int64_t wideNodes = 0;                  // node slots
     double wideBuildMs = 0.0;               // host build + upload, wall time
@@ -2038,10 +2044,13 @@ int buildWide(pt_scene* s) {
     for (int64_t k = 0; k < n; k++) std::memcpy(&wshade[(size_t)rank[k] * 12], &shade[(size_t)k * 12], 48);
     pt::Wide8 w;
     std::string err;
-    if (!pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, w, err)) return fail(PT_ERR_STATE, err);
+    const char* fl = std::getenv("PT_WIDE_FROM_LBVH");
+    const bool fromLbvh = fl && *fl == '1';
+    if (!pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, w, err, fromLbvh ? refs.data() : nullptr))
+        return fail(PT_ERR_STATE, err);
     int rc;
-    if ((rc = devAlloc(s->wide, w.nodes.size() * 4)) || (rc = devAlloc(s->wprims, w.prims.size() * 4)) ||
-        (rc = devAlloc(s->wshade, wshade.size() * 4)) || (rc = devAlloc(s->rankOf, rank.size() * 4)))
+    if ((rc = devReserve(s->wide, w.nodes.size() * 4)) || (rc = devReserve(s->wprims, w.prims.size() * 4)) ||
+        (rc = devReserve(s->wshade, wshade.size() * 4)) || (rc = devReserve(s->rankOf, rank.size() * 4)))
         return rc;
     HIP_TRY(hipMemcpy(s->wide.p, w.nodes.data(), w.nodes.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(s->wprims.p, w.prims.data(), w.prims.size() * 4, hipMemcpyHostToDevice));
@@ -2049,6 +2058,29 @@ int buildWide(pt_scene* s) {
     HIP_TRY(hipMemcpy(s->rankOf.p, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
     s->wideDepth = w.depth;
     s->wideNodes = (int64_t)(w.nodes.size() / pt::kW8NodeDwords);
+    s->wideSource = 1;
+    return PT_OK;
+}
+
+// The same records built on the device from the LBVH build's leaf records (csrc/pt_wide_build.hip),
+// enqueued on `st` (it synchronises with the stream once per clustering pass and wide level).
+int buildWideDevice(pt_scene* s, hipStream_t st) {
+    const int64_t n = s->nobj;
+    int rc;
+    if ((rc = devReserve(s->wide, (size_t)pt::wideDevNodeSlots(n) * pt::kW8NodeDwords * 4)) ||
+        (rc = devReserve(s->wprims, (size_t)n * pt::kW8PrimDwords * 4)) || (rc = devReserve(s->wshade, (size_t)n * 48)) ||
+        (rc = devReserve(s->rankOf, (size_t)n * 4)))
+        return rc;
+    if (!s->wideDev) s->wideDev.reset(new pt::WideDevBuilder);
+    pt::WideDevIn in{s->prims.as<float4>(), s->shade.as<float4>(), s->leafBoxes.as<float>(), s->nodes.as<float4>(),
+                     s->iparent.as<int>(), s->lparent.as<int>(), s->irange.as<int2>(), n};
+    pt::WideDevOut out{s->wide.as<uint32_t>(), s->wprims.as<uint32_t>(), s->wshade.as<float4>(), s->rankOf.as<uint32_t>()};
+    std::string err;
+    const hipError_t e = s->wideDev->build(in, out, st, err);
+    if (e != hipSuccess) return fail(err.empty() ? PT_ERR_HIP : PT_ERR_STATE, err.empty() ? hipGetErrorString(e) : err);
+    s->wideDepth = out.depth;
+    s->wideNodes = out.slots;
+    s->wideSource = 2;
     return PT_OK;
 }
 
@@ -2277,10 +2309,8 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     if (rc) return rc;
     const int64_t n = s->nobj;
     s->built = false;
-    s->wide.reset();
-    s->wprims.reset();
-    s->wshade.reset();
-    s->rankOf.reset();
+    s->wideReady = false;   // the wide buffers are kept for the next wide build
+    s->wideSource = 0;
     s->wideNodes = 0;
     s->wideDepth = 0;
     // Everything on the device, on one stream: scene box -> Morton codes -> radix sort ->
@@ -2290,7 +2320,7 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     if ((rc = devReserve(s->prims, n1 * 3 * sizeof(float4))) || (rc = devReserve(s->shade, n1 * 3 * sizeof(float4))) ||
         (rc = devReserve(s->nodes, ni * 4 * sizeof(float4))) || (rc = devReserve(s->keys, n1 * 8)) ||
         (rc = devReserve(s->leafBoxes, n1 * 24)) || (rc = devReserve(s->iparent, ni * 4)) ||
-        (rc = devReserve(s->lparent, n1 * 4)))
+        (rc = devReserve(s->lparent, n1 * 4)) || (rc = devReserve(s->irange, ni * 8)))
         return rc;
     DevBuf &codes = s->codes, &ids = s->ids, &codes2 = s->codes2, &ids2 = s->ids2, &box6 = s->box6, &sph = s->sph,
            &arr = s->arr, &dep = s->dep, &temp = s->sortTemp;
@@ -2339,13 +2369,19 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     HIP_TRY(hipMemsetAsync(dep.p, 0, 16, st));
     if (n > 1) {
         karrasKernel<<<nbi, tb, 0, st>>>(s->keys.as<unsigned long long>(), (int)n, s->nodes.as<float4>(),
-                                         s->iparent.as<int>(), s->lparent.as<int>(), sph.as<uint32_t>());
+                                         s->iparent.as<int>(), s->lparent.as<int>(), sph.as<uint32_t>(),
+                                         s->irange.as<int2>());
         HIP_TRY(hipGetLastError());
         refitKernel<<<nb, tb, 0, st>>>(s->nodes.as<float4>(), s->iparent.as<int>(), s->lparent.as<int>(),
                                        s->leafBoxes.as<float>(), arr.as<unsigned int>(), (int)n);
         HIP_TRY(hipGetLastError());
         depthKernel<<<nb, tb, 0, st>>>(s->iparent.as<int>(), s->lparent.as<int>(), (int)n, dep.as<int>());
         HIP_TRY(hipGetLastError());
+    }
+    if ((flags & PT_BVH_WIDE_DEVICE) && n > 0) {
+        if ((rc = buildWideDevice(s, st))) return rc;
+        s->wideReady = true;
+        s->wideBuildMs = 0.0;
     }
     HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));
@@ -2358,19 +2394,35 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     HIP_TRY(hipMemcpy(&depth, dep.p, 4, hipMemcpyDeviceToHost));
     s->depth = n > 1 ? depth : 0;
     if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
+    if (s->wideReady && wideStackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");
     s->deviceBytes = (size_t)(n > 1 ? n - 1 : 0) * 64 + (size_t)n * 96 + (size_t)s->nmat * 32;
     s->built = true;
     return PT_OK;
 }
 
-// The wide tree is only needed by PT_KERNEL_WIDE: built on first use after each LBVH build.
+// The wide tree is only needed by PT_KERNEL_WIDE: unless pt_scene_build_bvh built it on the
+// device (PT_BVH_WIDE_DEVICE), built on first use after each LBVH build -- on the host (binned
+// SAH), or on the device when PT_WIDE_BUILD=device.
 static int ensureWide(pt_scene* s) {
-    if (s->wide.p || s->nobj <= 0) return PT_OK;
+    if (s->wideReady || s->nobj <= 0) return PT_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    int rc = buildWide(s);
+    const char* wb = std::getenv("PT_WIDE_BUILD");
+    int rc = (wb && std::string(wb) == "device") ? buildWideDevice(s, 0) : buildWide(s);
+    if (!rc && s->wideSource == 2) HIP_TRY(hipStreamSynchronize(0));
     if (rc) return rc;
+    s->wideReady = true;
     s->wideBuildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (wideStackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");
+    return PT_OK;
+}
+
+int pt_scene_wide_info(pt_scene* s, int* depth, int64_t* slots, double* ms, int* source) {
+    if (!s) return fail(PT_ERR_INVALID, "pt_scene_wide_info: null scene");
+    const bool ok = s->wideReady;
+    if (depth) *depth = ok ? s->wideDepth : 0;
+    if (slots) *slots = ok ? s->wideNodes : 0;
+    if (ms) *ms = ok ? s->wideBuildMs : 0.0;
+    if (source) *source = ok ? s->wideSource : 0;
     return PT_OK;
 }
 

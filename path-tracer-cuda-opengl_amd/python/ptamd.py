@@ -21,7 +21,7 @@ MODELS_DIR = os.path.join(REPO, "models")
 PT_OK = 0
 PT_SPHERE, PT_TRIANGLE = 1, 3
 PT_LAMBERTIAN, PT_METAL, PT_DIELECTRIC = 1, 2, 4
-PT_BVH_ORIGIN_BOUNDS, PT_BVH_HOST_KEYS = 1, 2
+PT_BVH_ORIGIN_BOUNDS, PT_BVH_HOST_KEYS, PT_BVH_WIDE_DEVICE = 1, 2, 4
 
 # numpy mirrors of the C structs (all 4-byte fields, no padding)
 OBJECT_DTYPE = np.dtype([("type", "<i4"), ("mat", "<i4"), ("v", "<f4", (9,))])
@@ -77,7 +77,7 @@ EXPORTS = [
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
     "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
-    "pt_scene_update_objects", "pt_trace_closest_ex",
+    "pt_scene_update_objects", "pt_trace_closest_ex", "pt_scene_wide_info",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -105,6 +105,8 @@ _sig = {
     "pt_scene_update_objects": (C.c_int, [_P, _P, C.c_int64, C.c_int64]),
     "pt_scene_bvh_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "pt_scene_download_bvh": (C.c_int, [_P, _P]),
+    "pt_scene_wide_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_int)]),
     "pt_trace_closest": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, _P, C.POINTER(Stats)]),
     "pt_trace_closest_ex": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, C.c_int, _P, C.POINTER(Stats)]),
     "pt_film_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
@@ -265,6 +267,12 @@ class Scene:
         d, n, b = C.c_int(), C.c_int64(), C.c_int64()
         _check(lib.pt_scene_bvh_info(self.h, C.byref(d), C.byref(n), C.byref(b)), "pt_scene_bvh_info")
         return {"depth": d.value, "nodes": n.value, "device_bytes": b.value}
+
+    def wide_info(self) -> dict:
+        """The wide kernel's tree: depth, node slots, build ms, source (0 none yet, 1 host SAH, 2 device)."""
+        d, n, ms, src = C.c_int(), C.c_int64(), C.c_double(), C.c_int()
+        _check(lib.pt_scene_wide_info(self.h, C.byref(d), C.byref(n), C.byref(ms), C.byref(src)), "pt_scene_wide_info")
+        return {"depth": d.value, "slots": n.value, "build_ms": ms.value, "source": src.value}
 
     def download_bvh(self) -> np.ndarray:
         n = len(self.objects)

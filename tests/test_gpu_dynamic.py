@@ -10,7 +10,7 @@ Bar: bit-exact.
 import numpy as np
 import pytest
 
-from helpers import random_soup
+from helpers import random_rays, random_soup, rays_to_struct
 
 pytestmark = pytest.mark.gpu
 
@@ -125,3 +125,79 @@ def test_c5_rebuild_per_frame(pt, gpu):
     print(f"C5 build {first:.2f} ms, rebuilds {[round(t, 2) for t in times]} ms")
     assert scene.bvh_info()["nodes"] == 2 * len(p.objects) - 1
     assert max(times) < 50.0
+
+
+def test_wide_device_rebuild_per_frame(pt, orc, gpu):
+    """Moving objects rendered with the wide kernel, its tree rebuilt on the device every frame
+    (PT_BVH_WIDE_DEVICE): each frame equals the binary kernel's frame of a fresh scene and, for
+    compat streams, the oracle's render; the rebuild is deterministic (same stats twice)."""
+    flags = pt.PT_BVH_ORIGIN_BOUNDS | pt.PT_BVH_WIDE_DEVICE
+    objs0, mats = random_soup(600, 80, seed=31, spread=8.0)
+    scene = pt.Scene(objs0, mats, device=gpu, flags=flags)
+    cam = pt.camera_make((0, 2, 20), (0, 0, 0), 40.0, W / H)
+    for frame in (1, 2, 3):
+        objs = moved(pt, objs0, frame, np.random.default_rng(40 + frame))
+        scene.update_objects(objs)
+        scene.build_bvh(flags)
+        assert scene.wide_info()["source"] == 2
+        fresh = pt.Scene(objs, mats, device=gpu)
+        a, sa = pt.render(scene, pt.Film(W, H, seed=frame), cam, 2, 10, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE)
+        b, sb = pt.render(fresh, pt.Film(W, H, seed=frame), cam, 2, 10, kernel=pt.KERNEL_WAVEFRONT, rng=pt.RNG_SAMPLE)
+        np.testing.assert_array_equal(bits(a), bits(b))
+        assert sa.rays == sb.rays
+        scene.build_bvh(flags)   # same objects again: the same tree
+        a2, sa2 = pt.render(scene, pt.Film(W, H, seed=frame), cam, 2, 10, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE)
+        np.testing.assert_array_equal(bits(a2), bits(a))
+        assert (sa2.node_visits, sa2.tri_tests, sa2.sphere_tests) == (sa.node_visits, sa.tri_tests, sa.sphere_tests)
+    film = pt.Film(W, H, seed=9)
+    rgb, _ = pt.render(scene, film, cam, 2, 8, kernel=pt.KERNEL_WIDE)
+    nodes = orc.build_lbvh(objs, orc.morton_keys(objs), tight=True)
+    want, _, _ = orc.render_sums(objs, mats, nodes, pt.camera_to_array(cam), W, H, film.rows, 2, 8,
+                                 orc.film_states(9, W, film.rows), nthreads=8)
+    np.testing.assert_array_equal(bits(rgb), bits(want))
+
+
+def test_wide_device_identical_objects(pt, orc, gpu):
+    """5,000 copies of one triangle and 3,000 of one sphere: every clustering distance ties (the
+    pairing order must still halve the clusters each pass) and the reference's tie order decides
+    every hit."""
+    objs, mats = random_soup(1, 1, seed=50, n_mat=4)
+    tri, sph = objs[:1], objs[1:2]
+    assert tri["type"][0] == pt.PT_TRIANGLE and sph["type"][0] == pt.PT_SPHERE
+    rep = np.concatenate([np.repeat(tri, 5000), np.repeat(sph, 3000)])
+    rep["mat"] = np.arange(len(rep)) % 4
+    flags = pt.PT_BVH_ORIGIN_BOUNDS | pt.PT_BVH_WIDE_DEVICE
+    scene = pt.Scene(rep, mats, device=gpu, flags=flags)
+    info = scene.wide_info()
+    assert info["source"] == 2 and 1 <= info["depth"] <= 8
+    rays = random_rays(4096, seed=51, objects=rep)
+    hits, _ = scene.trace(rays_to_struct(rays, pt.RAY_DTYPE), 0.001, np.inf, kernel=pt.KERNEL_WIDE)
+    ref, _ = orc.trace(rep, orc.build_lbvh(rep, orc.morton_keys(rep), tight=True), rays, 0.001, np.inf)
+    for f in ("hit", "obj", "mat", "front_face"):
+        np.testing.assert_array_equal(hits[f], ref[f], err_msg=f)
+    h = hits["hit"] == 1
+    assert h.sum() > 100
+    for f in ("t", "p", "n"):
+        np.testing.assert_array_equal(bits(hits[f][h]), bits(ref[f][h]), err_msg=f)
+
+
+def test_c5_wide_device_rebuild(pt, gpu):
+    """1,043,312 triangles: LBVH + device wide tree per frame within a frame budget; the frame
+    equals the host-built wide tree's frame."""
+    p = pt.Preset("bunny_field", 160, 90)
+    flags = pt.PT_BVH_ORIGIN_BOUNDS | pt.PT_BVH_WIDE_DEVICE
+    scene = pt.Scene(p.objects, p.materials, device=gpu, flags=flags)
+    times = []
+    for frame in (1, 2):
+        objs = p.objects.copy()
+        objs["v"] += np.float32(0.01 * frame)
+        scene.update_objects(objs)
+        scene.build_bvh(flags)
+        times.append(scene.build_ms)
+    print(f"C5 LBVH + wide device rebuilds {[round(t, 2) for t in times]} ms, wide {scene.wide_info()}")
+    assert max(times) < 100.0
+    host = pt.Scene(objs, p.materials, device=gpu)
+    a, _ = pt.render(scene, pt.Film(160, 90, seed=3), p.camera, 2, p.max_depth, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE)
+    b, _ = pt.render(host, pt.Film(160, 90, seed=3), p.camera, 2, p.max_depth, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE)
+    assert host.wide_info()["source"] == 1
+    np.testing.assert_array_equal(bits(a), bits(b))

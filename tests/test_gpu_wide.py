@@ -4,6 +4,8 @@ The wide tree visits nodes in its own order (nearest child first) through conser
 8-bit quantised boxes; the closest hit is the minimum of (t, the reference's tie order), which is
 the hit the reference's left-first DFS keeps.  The bar is therefore the same as for the binary
 kernels: every hit record bit-exact, including exact ties (duplicated triangles and spheres).
+Every test runs on both trees: built on the host (binned SAH, at first use) and built on the
+device by pt_scene_build_bvh (PLOC + collapse, PT_BVH_WIDE_DEVICE).
 """
 import numpy as np
 import pytest
@@ -13,6 +15,19 @@ from helpers import OBJECT_DTYPE, MATERIAL_DTYPE, deep_stack_scene, random_rays,
 pytestmark = pytest.mark.gpu
 
 SCENES = ["triangle_world", "random_world", "test_world", "rtiow", "cornell", "bunny_cornell"]
+
+
+@pytest.fixture(params=["host", "device"])
+def wb(request):
+    return request.param
+
+
+def make_scene(pt, objs, mats, gpu, wb):
+    flags = pt.PT_BVH_ORIGIN_BOUNDS | (pt.PT_BVH_WIDE_DEVICE if wb == "device" else 0)
+    s = pt.Scene(objs, mats, device=gpu, flags=flags)
+    if wb == "device" and len(objs):
+        assert s.wide_info()["source"] == 2
+    return s
 
 
 def bits(a):
@@ -27,40 +42,41 @@ def assert_hits_equal(g, o):
         np.testing.assert_array_equal(bits(g[f][h]), bits(o[f][h]), err_msg=f)
 
 
-def trace_both(pt, orc, gpu, objs, mats, rays, tmin=0.001, tmax=np.inf):
-    s = pt.Scene(objs, mats, device=gpu)
+def trace_both(pt, orc, gpu, wb, objs, mats, rays, tmin=0.001, tmax=np.inf):
+    s = make_scene(pt, objs, mats, gpu, wb)
     hits, st = s.trace(rays_to_struct(rays, pt.RAY_DTYPE), tmin, tmax, kernel=pt.KERNEL_WIDE)
+    assert s.wide_info()["source"] == (2 if wb == "device" else 1)
     ref, rst = orc.trace(objs, orc.build_lbvh(objs, orc.morton_keys(objs), tight=True), rays, tmin, tmax)
     return hits, st, ref, rst
 
 
 @pytest.mark.parametrize("name", SCENES)
-def test_wide_trace_matches_oracle(pt, orc, gpu, name):
+def test_wide_trace_matches_oracle(pt, orc, gpu, wb, name):
     p = pt.Preset(name)
     lo = p.objects["v"][:, :3].min(0)
     hi = p.objects["v"][:, :3].max(0)
     center = np.clip((lo + hi) / 2, -1e3, 1e3)
     radius = float(min(np.linalg.norm(hi - lo), 3000.0)) * 0.75 + 1.0
     rays = random_rays(8192, seed=2, center=center, radius=radius, objects=p.objects)
-    hits, st, ref, rst = trace_both(pt, orc, gpu, p.objects, p.materials, rays)
+    hits, st, ref, rst = trace_both(pt, orc, gpu, wb, p.objects, p.materials, rays)
     assert_hits_equal(hits, ref)
     assert hits["hit"].sum() > 100
     assert st.rays == len(rays)
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_wide_trace_random_soup(pt, orc, gpu, seed):
+def test_wide_trace_random_soup(pt, orc, gpu, wb, seed):
     objs, mats = random_soup(3000, 500, seed=seed)
     rays = random_rays(8192, seed=seed + 10, objects=objs)
-    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
     assert_hits_equal(hits, ref)
 
 
-def test_wide_trace_tmin_tmax_window(pt, orc, gpu):
+def test_wide_trace_tmin_tmax_window(pt, orc, gpu, wb):
     objs, mats = random_soup(500, 100, seed=3)
     rays = random_rays(2048, seed=4, objects=objs)
     for tmin, tmax in ((0.001, 5.0), (2.0, 40.0), (0.0, np.inf)):
-        hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays, tmin, tmax)
+        hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays, tmin, tmax)
         assert_hits_equal(hits, ref)
 
 
@@ -76,47 +92,47 @@ def tie_scene(seed=5):
     return rep[perm], mats
 
 
-def test_wide_trace_exact_ties(pt, orc, gpu):
+def test_wide_trace_exact_ties(pt, orc, gpu, wb):
     objs, mats = tie_scene()
     rays = random_rays(8192, seed=6, objects=objs)
-    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
     assert_hits_equal(hits, ref)
     # the ties matter: the copies differ in material, and many rays hit a duplicated object
     assert (ref["hit"] == 1).sum() > 2000
 
 
-def test_wide_trace_coplanar_sphere_ties(pt, orc, gpu):
+def test_wide_trace_coplanar_sphere_ties(pt, orc, gpu, wb):
     """Concentric spheres of equal radius (the deep-stack scene: 2,048 identical spheres)."""
     objs, mats = deep_stack_scene(n_group=256)
     objs["mat"] = np.arange(len(objs)) % 1
     rays = random_rays(4096, seed=8, center=(1024.0, 1024.0, 1024.0), radius=3000.0, objects=objs)
-    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
     assert_hits_equal(hits, ref)
 
 
-def test_wide_trace_c5(pt, orc, gpu):
+def test_wide_trace_c5(pt, orc, gpu, wb):
     p = pt.Preset("bunny_field", 64, 36)
     rays = random_rays(8192, seed=9, center=(278, 150, 280), radius=700, objects=p.objects)
-    hits, st, ref, rst = trace_both(pt, orc, gpu, p.objects, p.materials, rays)
+    hits, st, ref, rst = trace_both(pt, orc, gpu, wb, p.objects, p.materials, rays)
     assert_hits_equal(hits, ref)
     assert st.node_visits < rst.node_visits   # the point of the wide tree
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 9])
-def test_wide_tiny_scenes(pt, orc, gpu, n):
+def test_wide_tiny_scenes(pt, orc, gpu, wb, n):
     """Roots that are a leaf (n <= 3) or a single wide node."""
     objs, mats = random_soup(n - n // 2, n // 2, seed=n)
     rays = random_rays(2048, seed=n, objects=objs)
-    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
     assert_hits_equal(hits, ref)
 
 
-def test_wide_render_ties_bit_exact(pt, orc, gpu):
+def test_wide_render_ties_bit_exact(pt, orc, gpu, wb):
     """A rendered frame of the tie scene: every bounce's hit must be the reference's copy."""
     objs, mats = tie_scene(seed=11)
     w, h = 48, 32
     cam = pt.camera_make((0.0, 0.0, 30.0), (0.0, 0.0, 0.0), 50.0, w / h)
-    s = pt.Scene(objs, mats, device=gpu)
+    s = make_scene(pt, objs, mats, gpu, wb)
     f = pt.Film(w, h, 5, device=gpu)
     nodes = orc.build_lbvh(objs, orc.morton_keys(objs), tight=True)
     for rng in ("compat", "sample"):
@@ -134,11 +150,11 @@ def test_wide_render_ties_bit_exact(pt, orc, gpu):
 
 
 @pytest.mark.parametrize("cfg,w,h,spp", [("bunny_cornell", 240, 135, 4), ("bunny_field", 160, 90, 2), ("cornell", 128, 128, 8)])
-def test_wide_frame_equals_reference_order_frame(pt, gpu, cfg, w, h, spp):
+def test_wide_frame_equals_reference_order_frame(pt, gpu, wb, cfg, w, h, spp):
     """Whole frames (both RNG modes) from the wide kernel equal the binary kernel's, which follows
     the reference's own visiting order (itself bit-exact against the oracle, test_gpu_parity.py)."""
     p = pt.Preset(cfg, w, h)
-    s = pt.Scene(p.objects, p.materials, device=gpu)
+    s = make_scene(pt, p.objects, p.materials, gpu, wb)
     for rng in (pt.RNG_COMPAT, pt.RNG_SAMPLE):
         out = {}
         for k in (pt.KERNEL_WAVEFRONT, pt.KERNEL_WIDE):
@@ -148,14 +164,14 @@ def test_wide_frame_equals_reference_order_frame(pt, gpu, cfg, w, h, spp):
         assert out[pt.KERNEL_WIDE][1].rays == out[pt.KERNEL_WAVEFRONT][1].rays
 
 
-def test_wide_large_soup_trace_and_render(pt, orc, gpu):
+def test_wide_large_soup_trace_and_render(pt, orc, gpu, wb):
     """200,000 random triangles and spheres: hit records against the oracle, and a frame against
     the reference-order kernel."""
     objs, mats = random_soup(150_000, 50_000, seed=12, spread=60.0)
     rays = random_rays(8192, seed=13, radius=90.0, objects=objs)
-    hits, _, ref, _ = trace_both(pt, orc, gpu, objs, mats, rays)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
     assert_hits_equal(hits, ref)
-    s = pt.Scene(objs, mats, device=gpu)
+    s = make_scene(pt, objs, mats, gpu, wb)
     cam = pt.camera_make((0.0, 20.0, 120.0), (0.0, 0.0, 0.0), 45.0, 1.5)
     frames = []
     for k in (pt.KERNEL_WAVEFRONT, pt.KERNEL_WIDE):
