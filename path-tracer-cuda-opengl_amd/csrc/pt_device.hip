@@ -2044,10 +2044,7 @@ int buildWide(pt_scene* s) {
     for (int64_t k = 0; k < n; k++) std::memcpy(&wshade[(size_t)rank[k] * 12], &shade[(size_t)k * 12], 48);
     pt::Wide8 w;
     std::string err;
-    const char* fl = std::getenv("PT_WIDE_FROM_LBVH");
-    const bool fromLbvh = fl && *fl == '1';
-    if (!pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, w, err, fromLbvh ? refs.data() : nullptr))
-        return fail(PT_ERR_STATE, err);
+    if (!pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, w, err)) return fail(PT_ERR_STATE, err);
     int rc;
     if ((rc = devReserve(s->wide, w.nodes.size() * 4)) || (rc = devReserve(s->wprims, w.prims.size() * 4)) ||
         (rc = devReserve(s->wshade, wshade.size() * 4)) || (rc = devReserve(s->rankOf, rank.size() * 4)))

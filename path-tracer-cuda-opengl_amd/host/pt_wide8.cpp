@@ -220,56 +220,8 @@ std::vector<uint32_t> referenceRanks(const uint32_t* leftRef, const uint32_t* ri
     return rank;
 }
 
-// The binary tree of the LBVH itself (refs: per internal node i its child refs at refs[i * 16 + 12],
-// refs[i * 16 + 13]): internal node i -> B node i, leaf k -> B node n - 1 + k; subtrees of at
-// most kMaxLeaf primitives (a contiguous Morton range) become one leaf.  Returns the root.
-int32_t lbvhTopology(SahBuilder& B, const uint32_t* refs, int64_t n) {
-    const uint32_t leafBit = 0x80000000u, mask = 0x3fffffffu;
-    const int32_t nIn = (int32_t)(n - 1);
-    auto node = [&](uint32_t r) { return (r & leafBit) ? nIn + (int32_t)(r & mask) : (int32_t)r; };
-    for (int64_t k = 0; k < n; k++) {
-        BNode& l = B.nodes[(size_t)(nIn + k)];
-        l.box = B.boxes[k];
-        l.first = (int32_t)k;
-        l.count = 1;
-    }
-    // post order: children before parents
-    std::vector<int32_t> order;
-    order.reserve((size_t)nIn);
-    std::vector<int32_t> st{0};
-    while (!st.empty()) {
-        const int32_t i = st.back();
-        st.pop_back();
-        order.push_back(i);
-        for (int c = 12; c < 14; c++) {
-            const uint32_t r = refs[(size_t)i * 16 + c];
-            if (!(r & leafBit)) st.push_back((int32_t)r);
-        }
-    }
-    std::vector<int32_t> cnt((size_t)(2 * n - 1), 1), lo((size_t)(2 * n - 1));
-    for (int64_t k = 0; k < n; k++) lo[(size_t)(nIn + k)] = (int32_t)k;
-    for (size_t o = order.size(); o-- > 0;) {
-        const int32_t i = order[o];
-        const int32_t l = node(refs[(size_t)i * 16 + 12]), r = node(refs[(size_t)i * 16 + 13]);
-        BNode& nd = B.nodes[(size_t)i];
-        nd.box = B.nodes[(size_t)l].box;
-        growBox(nd.box, B.nodes[(size_t)r].box);
-        cnt[i] = cnt[l] + cnt[r];
-        lo[i] = std::min(lo[l], lo[r]);
-        if (cnt[i] <= B.kMaxLeaf) {   // Karras ranges are contiguous in leaf order
-            nd.first = lo[i];
-            nd.count = cnt[i];
-        } else {
-            nd.left = l;
-            nd.right = r;
-            nd.count = 0;
-        }
-    }
-    return 0;
-}
-
 bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
-                std::string& err, const uint32_t* lbvhRefs) {
+                std::string& err) {
     out = Wide8{};
     if (n <= 0) return true;
     if (n >= (int64_t)1 << 26) {
@@ -288,7 +240,7 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
     }
     B.nodes.resize((size_t)(2 * n));
     B.maxThreads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const int32_t root = lbvhRefs && n > 1 ? lbvhTopology(B, lbvhRefs, n) : B.build(0, (int32_t)n);
+    const int32_t root = B.build(0, (int32_t)n);
     const BBox rootBox = B.nodes[root].box;
 
     // Smallest plane quantum: far below any box of interest, far above the rounding of the

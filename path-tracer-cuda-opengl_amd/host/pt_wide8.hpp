@@ -30,10 +30,8 @@ struct Wide8 {
 // ({v0, rank}...): ties between equal hit distances are decided by it, and it indexes the wide
 // kernels' shading records.  Returns false with `err` set when the tree exceeds the encoding
 // limits.
-// lbvhRefs (optional): collapse the binary LBVH itself (the device node array: per internal node
-// 16 dwords, child refs at dwords 12 and 13) instead of building a binned-SAH tree.
 bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
-                std::string& err, const uint32_t* lbvhRefs = nullptr);
+                std::string& err);
 
 // The order in which RenderManager::hitBvh (render_manager.h:105-133) would test the leaves of
 // the binary LBVH if every box passed: at a node, its leaf children (left, then right), then the
