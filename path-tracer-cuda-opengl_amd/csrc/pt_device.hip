@@ -1712,31 +1712,32 @@ __global__ void karrasKernel(const unsigned long long* __restrict__ keys, int n,
     irange[i] = make_int2(first, last);   // leaf range (the device wide build's ranks)
 }
 
-// Writes a child box into slot (0 = left, 1 = right) of node p with write-through stores.
-__device__ __forceinline__ void storeBox(float4* nodes, int p, int slot, const float b[6]) {
-    float* f = reinterpret_cast<float*>(nodes + 4 * (size_t)p);
-#pragma unroll
-    for (int i = 0; i < 6; i++)   // b = {min xyz, max xyz}
-        __hip_atomic_store(f + nodeBoxIdx(slot, i % 3, i / 3), b[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void loadBox(const float4* nodes, int p, int slot, float b[6]) {
-    const float* f = reinterpret_cast<const float*>(nodes + 4 * (size_t)p);
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-        b[i] = __hip_atomic_load(f + nodeBoxIdx(slot, i % 3, i / 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // growBBox (bvh.h:117-130) as a correct bottom-up refit: every leaf writes its box into its
-// parent's slot, then climbs; the second thread to reach a node (agent-scope acq_rel counter)
-// unions the node's two child boxes into the grandparent's slot.  Tight boxes.
-__global__ void refitKernel(float4* nodes, const int* __restrict__ iparent, const int* __restrict__ lparent,
-                            const float* __restrict__ leafBoxes, unsigned int* arrivals, int n) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+// parent's slot, then climbs; the second thread to reach a node unions the node's two child boxes
+// into the grandparent's slot.  Tight boxes.
+//
+// No agent-scope synchronisation (its acq_rel fence is an L2 writeback + invalidate on this
+// multi-L2 chip: the all-global version spent 3.7 ms of a 5-ms C5 build in them).  Phase 1: a
+// workgroup owns the 256 leaves [base, base + 256); a node whose leaf range lies inside them
+// (Karras: node i is an end of its own range, so i is in the block too) is completed in LDS with
+// workgroup-scope counters.  A thread reaching a node whose range crosses a block boundary
+// stores its box in that node's slot and records the arrival (events).  Phase 2: one workgroup
+// replays the arrivals with workgroup-scope counters in global memory -- the crossing nodes are
+// the top of the tree, about 1/16 of the nodes.
+constexpr int kRefitBlock = 256, kRefitTop = 1024;
+__global__ __launch_bounds__(kRefitBlock) void refitKernel(float4* nodes, const int* __restrict__ iparent,
+                                                           const int* __restrict__ lparent, const int2* __restrict__ irange,
+                                                           const float* __restrict__ leafBoxes, unsigned int* events, int n) {
+    __shared__ float sbox[kRefitBlock][2][6];   // child boxes of the block's internal nodes
+    __shared__ unsigned int scnt[kRefitBlock];
+    const int base = blockIdx.x * kRefitBlock, end = min(base + kRefitBlock, n);
+    scnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const int k = base + (int)threadIdx.x;
     if (k >= n) return;
     float b[6];
     for (int i = 0; i < 6; i++) b[i] = leafBoxes[6 * (size_t)k + i];
     int p = lparent[k];
-    uint32_t childRef = kLeafBit;   // compare on the index bits only
     int self = k;
     bool leaf = true;
     for (int guard = 0; p >= 0 && guard < 130; guard++) {
@@ -1744,22 +1745,49 @@ __global__ void refitKernel(float4* nodes, const int* __restrict__ iparent, cons
         const uint32_t lref = __float_as_uint(refs.x);
         const bool isLeft = leaf ? ((lref & kLeafBit) && (int)(lref & kPrimMask) == self)
                                  : (!(lref & kLeafBit) && (int)lref == self);
-        storeBox(nodes, p, isLeft ? 0 : 1, b);
-        const unsigned int prev =
-            __hip_atomic_fetch_add(arrivals + p, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        float* f = reinterpret_cast<float*>(nodes + 4 * (size_t)p);
+        for (int i = 0; i < 6; i++) f[nodeBoxIdx(isLeft ? 0 : 1, i % 3, i / 3)] = b[i];
+        const int2 range = irange[p];
+        if (range.x < base || range.y >= end) {   // crossing: phase 2 finishes it
+            events[1 + atomicAdd(events, 1u)] = (unsigned)p;
+            return;
+        }
+        for (int i = 0; i < 6; i++) sbox[p - base][isLeft ? 0 : 1][i] = b[i];
+        const unsigned int prev = __hip_atomic_fetch_add(&scnt[p - base], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (prev == 0) return;   // sibling not done yet: it will carry on
-        float l6[6], r6[6];
-        loadBox(nodes, p, 0, l6);
-        loadBox(nodes, p, 1, r6);
         for (int i = 0; i < 3; i++) {   // utils::unionBox (aabb.h:55-65)
-            b[i] = fminf(l6[i], r6[i]);
-            b[3 + i] = fmaxf(l6[3 + i], r6[3 + i]);
+            b[i] = fminf(sbox[p - base][0][i], sbox[p - base][1][i]);
+            b[3 + i] = fmaxf(sbox[p - base][0][3 + i], sbox[p - base][1][3 + i]);
         }
         self = p;
         leaf = false;
         p = iparent[p];
     }
-    (void)childRef;
+}
+
+__global__ __launch_bounds__(kRefitTop) void refitTopKernel(float4* nodes, const int* __restrict__ iparent,
+                                                            const unsigned int* __restrict__ events, unsigned int* arrivals) {
+    const unsigned int count = events[0];
+    for (unsigned int e = threadIdx.x; e < count; e += kRefitTop) {
+        int p = (int)events[1 + e];
+        for (int guard = 0; p >= 0 && guard < 130; guard++) {
+            const unsigned int prev = __hip_atomic_fetch_add(arrivals + p, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (prev == 0) break;   // the other child is not done yet
+            const float* f = reinterpret_cast<const float*>(nodes + 4 * (size_t)p);
+            float b[6];
+            for (int i = 0; i < 3; i++) {   // utils::unionBox (aabb.h:55-65)
+                b[i] = fminf(f[nodeBoxIdx(0, i, 0)], f[nodeBoxIdx(1, i, 0)]);
+                b[3 + i] = fmaxf(f[nodeBoxIdx(0, i, 1)], f[nodeBoxIdx(1, i, 1)]);
+            }
+            const int q = iparent[p];
+            if (q < 0) break;
+            const uint32_t lref = __float_as_uint(nodes[4 * (size_t)q + 3].x);
+            const bool isLeft = !(lref & kLeafBit) && (int)lref == p;
+            float* g = reinterpret_cast<float*>(nodes + 4 * (size_t)q);
+            for (int i = 0; i < 6; i++) g[nodeBoxIdx(isLeft ? 0 : 1, i % 3, i / 3)] = b[i];
+            p = q;
+        }
+    }
 }
 
 // --- Morton keys and leaf records on the device (morton_code.h:19-75, cuda_object.h:21-42) ----
@@ -1787,22 +1815,37 @@ __device__ __forceinline__ void objBoxDev(const pt_object& o, float mn[3], float
 
 // Scene box for the Morton quantisation (main.cu:122 + aabb::unionBoxInPlace, aabb.h:36-44):
 // min/max are exact and order-independent, so one workgroup reduces all boxes.  The reference
-// seeds the box with aabb() = the zero box (includeOrigin), or the first object's box.
+// seeds the box with aabb() = the zero box (includeOrigin), or the first object's box.  Two
+// launches: per-block boxes over a grid-stride range (partial[6 * block]), then their union.
+constexpr int kBoxBlocks = 512;
 __global__ __launch_bounds__(1024) void sceneBoxKernel(const pt_object* __restrict__ objs, int64_t n,
-                                                       int includeOrigin, float* box6) {
+                                                       int includeOrigin, float* box6, float* partial) {
     __shared__ float red[6][1024];
     float b[6];
-    if (includeOrigin) {
-        for (int a = 0; a < 6; a++) b[a] = 0.0f;
+    const bool final = partial == nullptr;   // the second launch: union of the per-block boxes in box6 + 6
+    if (final || includeOrigin) {
+        for (int a = 0; a < 6; a++) b[a] = final ? (a < 3 ? INFINITY : -INFINITY) : 0.0f;
+        if (final && includeOrigin)
+            for (int a = 0; a < 6; a++) b[a] = 0.0f;
     } else {
         objBoxDev(objs[0], b, b + 3);
     }
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        float mn[3], mx[3];
-        objBoxDev(objs[i], mn, mx);
-        for (int a = 0; a < 3; a++) {
-            b[a] = fminf(b[a], mn[a]);
-            b[3 + a] = fmaxf(b[3 + a], mx[a]);
+    if (final) {
+        const float* pb = box6 + 6;
+        if (!includeOrigin && threadIdx.x == 0) objBoxDev(objs[0], b, b + 3);
+        for (int i = threadIdx.x; i < kBoxBlocks; i += blockDim.x)
+            for (int a = 0; a < 3; a++) {
+                b[a] = fminf(b[a], pb[6 * i + a]);
+                b[3 + a] = fmaxf(b[3 + a], pb[6 * i + 3 + a]);
+            }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+            float mn[3], mx[3];
+            objBoxDev(objs[i], mn, mx);
+            for (int a = 0; a < 3; a++) {
+                b[a] = fminf(b[a], mn[a]);
+                b[3 + a] = fmaxf(b[3 + a], mx[a]);
+            }
         }
     }
     for (int a = 0; a < 6; a++) red[a][threadIdx.x] = b[a];
@@ -1815,7 +1858,7 @@ __global__ __launch_bounds__(1024) void sceneBoxKernel(const pt_object* __restri
             }
         __syncthreads();
     }
-    if (threadIdx.x < 6) box6[threadIdx.x] = red[threadIdx.x][0];
+    if (threadIdx.x < 6) (final ? box6 : partial + 6 * blockIdx.x)[threadIdx.x] = red[threadIdx.x][0];
 }
 
 __device__ __forceinline__ uint32_t expandBitsDev(uint32_t v) {   // morton_code.h:19-27
@@ -1992,6 +2035,7 @@ struct pt_scene {
     // flags, refit arrival counters, depth, sort temporary
     DevBuf codes, ids, codes2, ids2, box6, sph, arr, dep, sortTemp;
     DevBuf irange;                          // leaf range [first, last] per internal node
+    DevBuf refitEvents;                     // refit phase 2 input: count, then crossing-node arrivals
     DevBuf wide, wprims, wshade, rankOf;    // compressed 8-wide tree, its primitive and shading records, leaf ranks (PT_KERNEL_WIDE)
     std::unique_ptr<pt::WideDevBuilder> wideDev;   // device build scratch (PT_BVH_WIDE_DEVICE), kept between builds
     bool wideReady = false;                 // the wide tree matches the current LBVH build
@@ -2317,12 +2361,13 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     if ((rc = devReserve(s->prims, n1 * 3 * sizeof(float4))) || (rc = devReserve(s->shade, n1 * 3 * sizeof(float4))) ||
         (rc = devReserve(s->nodes, ni * 4 * sizeof(float4))) || (rc = devReserve(s->keys, n1 * 8)) ||
         (rc = devReserve(s->leafBoxes, n1 * 24)) || (rc = devReserve(s->iparent, ni * 4)) ||
-        (rc = devReserve(s->lparent, n1 * 4)) || (rc = devReserve(s->irange, ni * 8)))
+        (rc = devReserve(s->lparent, n1 * 4)) || (rc = devReserve(s->irange, ni * 8)) ||
+        (rc = devReserve(s->refitEvents, (ni + 1) * 4)))
         return rc;
     DevBuf &codes = s->codes, &ids = s->ids, &codes2 = s->codes2, &ids2 = s->ids2, &box6 = s->box6, &sph = s->sph,
            &arr = s->arr, &dep = s->dep, &temp = s->sortTemp;
     if ((rc = devReserve(codes, n1 * 4)) || (rc = devReserve(ids, n1 * 4)) || (rc = devReserve(codes2, n1 * 4)) ||
-        (rc = devReserve(ids2, n1 * 4)) || (rc = devReserve(box6, 64)) || (rc = devReserve(sph, n1 * 4)) ||
+        (rc = devReserve(ids2, n1 * 4)) || (rc = devReserve(box6, (1 + kBoxBlocks) * 6 * sizeof(float))) || (rc = devReserve(sph, n1 * 4)) ||
         (rc = devReserve(arr, ni * 4)) || (rc = devReserve(dep, 16)))
         return rc;
     hipStream_t st = 0;
@@ -2341,8 +2386,10 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
             HIP_TRY(hipMemcpyAsync(ids2.p, hi.data(), n * 4, hipMemcpyHostToDevice, st));
             HIP_TRY(hipStreamSynchronize(st));
         } else {
-            sceneBoxKernel<<<1, 1024, 0, st>>>(s->dobjs.as<pt_object>(), n, (flags & PT_BVH_ORIGIN_BOUNDS) ? 1 : 0,
-                                               box6.as<float>());
+            const int inc = (flags & PT_BVH_ORIGIN_BOUNDS) ? 1 : 0;
+            sceneBoxKernel<<<kBoxBlocks, 1024, 0, st>>>(s->dobjs.as<pt_object>(), n, inc, box6.as<float>(),
+                                                        box6.as<float>() + 6);
+            sceneBoxKernel<<<1, 1024, 0, st>>>(s->dobjs.as<pt_object>(), n, inc, box6.as<float>(), nullptr);
             mortonKernel<<<nb, tb, 0, st>>>(s->dobjs.as<pt_object>(), n, box6.as<float>(), codes.as<uint32_t>(),
                                             ids.as<uint32_t>());
             HIP_TRY(hipGetLastError());
@@ -2363,14 +2410,18 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     HIP_TRY(hipMemsetAsync(s->iparent.p, 0xff, ni * 4, st));
     HIP_TRY(hipMemsetAsync(s->lparent.p, 0xff, n1 * 4, st));
     HIP_TRY(hipMemsetAsync(arr.p, 0, ni * 4, st));
+    HIP_TRY(hipMemsetAsync(s->refitEvents.p, 0, 4, st));
     HIP_TRY(hipMemsetAsync(dep.p, 0, 16, st));
     if (n > 1) {
         karrasKernel<<<nbi, tb, 0, st>>>(s->keys.as<unsigned long long>(), (int)n, s->nodes.as<float4>(),
                                          s->iparent.as<int>(), s->lparent.as<int>(), sph.as<uint32_t>(),
                                          s->irange.as<int2>());
         HIP_TRY(hipGetLastError());
-        refitKernel<<<nb, tb, 0, st>>>(s->nodes.as<float4>(), s->iparent.as<int>(), s->lparent.as<int>(),
-                                       s->leafBoxes.as<float>(), arr.as<unsigned int>(), (int)n);
+        refitKernel<<<(unsigned)((n + kRefitBlock - 1) / kRefitBlock), kRefitBlock, 0, st>>>(
+            s->nodes.as<float4>(), s->iparent.as<int>(), s->lparent.as<int>(), s->irange.as<int2>(),
+            s->leafBoxes.as<float>(), s->refitEvents.as<unsigned int>(), (int)n);
+        refitTopKernel<<<1, kRefitTop, 0, st>>>(s->nodes.as<float4>(), s->iparent.as<int>(),
+                                                s->refitEvents.as<unsigned int>(), arr.as<unsigned int>());
         HIP_TRY(hipGetLastError());
         depthKernel<<<nb, tb, 0, st>>>(s->iparent.as<int>(), s->lparent.as<int>(), (int)n, dep.as<int>());
         HIP_TRY(hipGetLastError());

@@ -32,7 +32,10 @@ constexpr int kRadiusDefault = 8;              // PLOC neighbourhood (positions 
 constexpr int kTile = 256;
 constexpr int kMaxGroup = 3;                   // primitives per leaf (the meta byte's unary count)
 constexpr int kMaxLevels = 24;                 // the wide kernels' deepest traversal stack
-enum { kMiscNodes = 0, kMiscM = 1, kMiscTotA = 2, kMiscTotB = 3, kMiscTotC = 4, kMiscErr = 5, kMiscWords = 8 };
+// device scalars: node counter, cluster count (two slots: a pass reads one, writes the other),
+// a level's totals and the error flags (read by the host in one copy)
+enum { kMiscNodes = 0, kMiscM = 1, kMiscTotA = 3, kMiscTotB = 4, kMiscTotC = 5, kMiscErr = 6, kMiscWords = 8 };
+constexpr int kPassesPerSync = 4;              // PLOC passes enqueued per host read of the cluster count
 
 __device__ __forceinline__ float areaOf(float4 lo, float4 hi) {
     const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
@@ -94,9 +97,12 @@ __global__ void plocInitKernel(const float* __restrict__ leafBoxes, int n, float
     cid[k] = (uint32_t)k;
 }
 
+// The PLOC kernels read the cluster count m from the device (several passes run between two
+// host reads; the grid covers the count the host last read, an upper bound).
 template <int kRadius>
 __global__ __launch_bounds__(kTile) void plocNearestKernel(const uint32_t* __restrict__ cid, const float4* __restrict__ pbox,
-                                                           int m, int* nn) {
+                                                           const uint32_t* __restrict__ mDev, int* nn) {
+    const int m = (int)*mDev;
     __shared__ float4 tlo[kTile + 2 * kRadius], thi[kTile + 2 * kRadius];
     const int base = blockIdx.x * kTile - kRadius;
     for (int t = threadIdx.x; t < kTile + 2 * kRadius; t += kTile) {
@@ -134,10 +140,16 @@ __global__ __launch_bounds__(kTile) void plocNearestKernel(const uint32_t* __res
     nn[i] = best;
 }
 
-__global__ void plocMergeKernel(uint32_t* cid, float4* pbox, uint2* pchild, const int* __restrict__ nn, int m, int n,
-                                float kTravCost, uint32_t* flag, uint32_t* misc) {
+__global__ void plocMergeKernel(uint32_t* cid, float4* pbox, uint2* pchild, const int* __restrict__ nn,
+                                const uint32_t* __restrict__ mDev, int mGrid, int n, float kTravCost, uint32_t* flag,
+                                uint32_t* misc) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
+    const int m = (int)*mDev;
+    if (i >= mGrid) return;
+    if (i >= m) {   // the scan runs over the grid's range
+        flag[i] = 0u;
+        return;
+    }
     const int j = nn[i];
     if (j < 0 || nn[j] != i) {
         flag[i] = 1u;
@@ -165,11 +177,13 @@ __global__ void plocMergeKernel(uint32_t* cid, float4* pbox, uint2* pchild, cons
 }
 
 __global__ void plocCompactKernel(const uint32_t* __restrict__ cid, const uint32_t* __restrict__ flag,
-                                  const uint32_t* __restrict__ pos, int m, uint32_t* out, uint32_t* misc) {
+                                  const uint32_t* __restrict__ pos, const uint32_t* __restrict__ mDev, uint32_t* out,
+                                  uint32_t* mNext) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = (int)*mDev;
     if (i >= m) return;
     if (flag[i]) out[pos[i]] = cid[i];
-    if (i == m - 1) misc[kMiscM] = pos[i] + flag[i];
+    if (i == m - 1) *mNext = pos[i] + flag[i];
 }
 
 // ---------------------------------------------------------------------------------- collapse
@@ -501,32 +515,40 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
     WB_TRY(hipGetLastError());
     int cur = 0;
     int64_t m = n;
-    for (int pass = 0; m > 1; pass++) {
+    {
+        const uint32_t m0 = (uint32_t)n;
+        WB_TRY(hipMemcpyAsync(misc + kMiscM, &m0, 4, hipMemcpyHostToDevice, st));
+    }
+    for (int pass = 0; m > 1;) {
         if (pass > 4 * 64 + 64) {
             err = "wide BVH (device): clustering does not converge";
             return hipErrorUnknown;
         }
-        uint32_t* cid = static_cast<uint32_t*>(cid_[cur].p);
-        switch (radius) {
-            case 8: plocNearestKernel<8><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, (int)m, nearest); break;
-            case 32: plocNearestKernel<32><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, (int)m, nearest); break;
-            case 64: plocNearestKernel<64><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, (int)m, nearest); break;
-            default: plocNearestKernel<16><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, (int)m, nearest); break;
+        for (int b = 0; b < kPassesPerSync; b++, pass++) {
+            uint32_t* cid = static_cast<uint32_t*>(cid_[cur].p);
+            const uint32_t* mIn = misc + kMiscM + (pass & 1);
+            switch (radius) {
+                case 8: plocNearestKernel<8><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, mIn, nearest); break;
+                case 32: plocNearestKernel<32><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, mIn, nearest); break;
+                case 64: plocNearestKernel<64><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, mIn, nearest); break;
+                default: plocNearestKernel<16><<<blocks(m, kTile), kTile, 0, st>>>(cid, pbox, mIn, nearest); break;
+            }
+            plocMergeKernel<<<blocks(m, tb), tb, 0, st>>>(cid, pbox, pchild, nearest, mIn, (int)m, (int)n, trav, flag, misc);
+            WB_TRY(hipGetLastError());
+            WB_TRY(rocprim::exclusive_scan(scanTemp_.p, tbytes, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
+            plocCompactKernel<<<blocks(m, tb), tb, 0, st>>>(cid, flag, pos, mIn, static_cast<uint32_t*>(cid_[cur ^ 1].p),
+                                                            misc + kMiscM + ((pass + 1) & 1));
+            WB_TRY(hipGetLastError());
+            cur ^= 1;
         }
-        plocMergeKernel<<<blocks(m, tb), tb, 0, st>>>(cid, pbox, pchild, nearest, (int)m, (int)n, trav, flag, misc);
-        WB_TRY(hipGetLastError());
-        WB_TRY(rocprim::exclusive_scan(scanTemp_.p, tbytes, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
-        plocCompactKernel<<<blocks(m, tb), tb, 0, st>>>(cid, flag, pos, (int)m, static_cast<uint32_t*>(cid_[cur ^ 1].p), misc);
-        WB_TRY(hipGetLastError());
         uint32_t mNext = 0;
-        WB_TRY(hipMemcpyAsync(&mNext, misc + kMiscM, 4, hipMemcpyDeviceToHost, st));
+        WB_TRY(hipMemcpyAsync(&mNext, misc + kMiscM + (pass & 1), 4, hipMemcpyDeviceToHost, st));
         WB_TRY(hipStreamSynchronize(st));
         if ((int64_t)mNext >= m) {
-            err = "wide BVH (device): a clustering pass merged nothing";
+            err = "wide BVH (device): clustering passes merged nothing";
             return hipErrorUnknown;
         }
         m = mNext;
-        cur ^= 1;
     }
     const uint32_t* rootCid = static_cast<const uint32_t*>(cid_[cur].p);
 

@@ -368,7 +368,7 @@ def test_lpt_tile_order_is_result_neutral(pt, gpu):
 def render_sample_both(pt, orc, gpu, p, w, h, spp, depth, seed, chunk, **kw):
     s = pt.Scene(p.objects, p.materials, device=gpu)
     f = pt.Film(w, h, seed, device=gpu, **kw)
-    rgb, st = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk)
+    rgb, st = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk, kernel=pt.KERNEL_WAVEFRONT)
     nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
     ref, rst = orc.render_sample(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, f.rows, spp,
                                  depth, seed, chunk or max(16, -(-spp // 64)), nthreads=8)
