@@ -140,26 +140,10 @@ __global__ __launch_bounds__(kTile) void plocNearestKernel(const uint32_t* __res
     nn[i] = best;
 }
 
-__global__ void plocMergeKernel(uint32_t* cid, float4* pbox, uint2* pchild, const int* __restrict__ nn,
-                                const uint32_t* __restrict__ mDev, int mGrid, int n, float kTravCost, uint32_t* flag,
-                                uint32_t* misc) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int m = (int)*mDev;
-    if (i >= mGrid) return;
-    if (i >= m) {   // the scan runs over the grid's range
-        flag[i] = 0u;
-        return;
-    }
-    const int j = nn[i];
-    if (j < 0 || nn[j] != i) {
-        flag[i] = 1u;
-        return;
-    }
-    if (i > j) {   // merged into position j
-        flag[i] = 0u;
-        return;
-    }
-    const uint32_t a = cid[i], b = cid[j];
+// The merged node of the clusters at positions i < j (ids a, b): box, primitive count, SAH cost
+// and the leaf decision (count x area vs traversal x area + the children's costs).
+__device__ __forceinline__ void makeNode(float4* pbox, uint2* pchild, uint32_t n, uint32_t id, uint32_t a, uint32_t b,
+                                         float kTravCost) {
     const float4 la = pbox[2 * (size_t)a], ha = pbox[2 * (size_t)a + 1];
     const float4 lb = pbox[2 * (size_t)b], hb = pbox[2 * (size_t)b + 1];
     const float4 lo = minBox(la, lb), hi = maxBox(ha, hb);
@@ -168,12 +152,114 @@ __global__ void plocMergeKernel(uint32_t* cid, float4* pbox, uint2* pchild, cons
     const float split = kTravCost * area + la.w + lb.w;
     const float asLeaf = count <= (uint32_t)kMaxGroup ? (float)count * area : INFINITY;
     const bool group = asLeaf <= split;
-    const uint32_t id = (uint32_t)n + atomicAdd(misc + kMiscNodes, 1u);
     pbox[2 * (size_t)id] = make_float4(lo.x, lo.y, lo.z, group ? asLeaf : split);
     pbox[2 * (size_t)id + 1] = make_float4(hi.x, hi.y, hi.z, __uint_as_float(count | (group ? kGroupFlag : 0u)));
-    pchild[id - (uint32_t)n] = make_uint2(a, b);
+    pchild[id - n] = make_uint2(a, b);
+}
+
+__global__ void plocMergeKernel(uint32_t* cid, float4* pbox, uint2* pchild, const int* __restrict__ nn,
+                                const uint32_t* __restrict__ mDev, int mGrid, int n, float kTravCost, uint32_t* flag,
+                                uint32_t* misc) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = (int)*mDev;
+    const int j = i < m ? nn[i] : -1;
+    const bool mutual = j >= 0 && nn[j] == i;
+    const bool merge = mutual && i < j;
+    // node ids: one counter add per wave
+    const uint64_t mask = __ballot(merge);
+    uint32_t base = 0;
+    if (mask) {
+        const int leader = __builtin_ctzll(mask);
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(misc + kMiscNodes, (uint32_t)__popcll(mask));
+        base = __shfl(base, leader);
+    }
+    if (i >= mGrid) return;
+    // flags: 1 = the position survives (0 beyond m: the scan runs over the grid's range)
+    flag[i] = (i < m && !(mutual && i > j)) ? 1u : 0u;
+    if (!merge) return;
+    const uint32_t id = (uint32_t)n + base + (uint32_t)__popcll(mask & ((1ull << (threadIdx.x & 63)) - 1ull));
+    makeNode(pbox, pchild, (uint32_t)n, id, cid[i], cid[j], kTravCost);
     cid[i] = id;
-    flag[i] = 1u;
+}
+
+// The last passes (m <= kTailMax clusters) in one workgroup: no launches or host reads per pass.
+constexpr int kTailThreads = 1024, kTailMax = 16384;
+template <int kRadius>
+__global__ __launch_bounds__(kTailThreads) void plocTailKernel(uint32_t* cidA, uint32_t* cidB, float4* pbox, uint2* pchild,
+                                                               int* nn, uint32_t* flag, const uint32_t* __restrict__ mDev,
+                                                               uint32_t* misc, int n, float kTravCost) {
+    __shared__ uint32_t sNodes, sM, sums[kTailThreads];
+    const int t = threadIdx.x;
+    if (t == 0) {
+        sNodes = misc[kMiscNodes];
+        sM = *mDev;
+    }
+    __syncthreads();
+    uint32_t* cur = cidA;
+    uint32_t* nxt = cidB;
+    int m = (int)sM;
+    while (m > 1) {
+        for (int i = t; i < m; i += kTailThreads) {   // nearest neighbour (the same rule as plocNearestKernel)
+            const uint32_t ci = cur[i];
+            const float4 lo = pbox[2 * (size_t)ci], hi = pbox[2 * (size_t)ci + 1];
+            int best = -1;
+            float bestA = INFINITY;
+            uint64_t bestKey = ~0ull;
+            for (int o = -kRadius; o <= kRadius; o++) {
+                const int j = i + o;
+                if (o == 0 || j < 0 || j >= m) continue;
+                const uint32_t cj = cur[j];
+                const float a = areaOf(minBox(lo, pbox[2 * (size_t)cj]), maxBox(hi, pbox[2 * (size_t)cj + 1]));
+                const int mn = o < 0 ? j : i;
+                const uint64_t key = ((uint64_t)(o < 0 ? -o : o) << 27) | ((uint64_t)(mn & 1) << 26) | (uint64_t)mn;
+                if (a < bestA || (a == bestA && key < bestKey)) {
+                    bestA = a;
+                    bestKey = key;
+                    best = j;
+                }
+            }
+            nn[i] = best;
+        }
+        __syncthreads();
+        for (int i = t; i < m; i += kTailThreads) {   // merges
+            const int j = nn[i];
+            const bool mutual = j >= 0 && nn[j] == i;
+            flag[i] = (mutual && i > j) ? 0u : 1u;
+            if (mutual && i < j) {
+                const uint32_t id = (uint32_t)n + atomicAdd(&sNodes, 1u);
+                makeNode(pbox, pchild, (uint32_t)n, id, cur[i], cur[j], kTravCost);
+                cur[i] = id;
+            }
+        }
+        __syncthreads();
+        // compaction in order: thread t owns the contiguous chunk [t * c, (t + 1) * c)
+        const int c = (m + kTailThreads - 1) / kTailThreads;
+        const int lo = min(m, t * c), hi = min(m, lo + c);
+        uint32_t cnt = 0;
+        for (int i = lo; i < hi; i++) cnt += flag[i];
+        sums[t] = cnt;
+        __syncthreads();
+        for (int off = 1; off < kTailThreads; off <<= 1) {   // inclusive scan of the chunk counts
+            const uint32_t v = t >= off ? sums[t - off] : 0u;
+            __syncthreads();
+            sums[t] += v;
+            __syncthreads();
+        }
+        uint32_t pos = sums[t] - cnt;
+        for (int i = lo; i < hi; i++)
+            if (flag[i]) nxt[pos++] = cur[i];
+        const int mNext = (int)sums[kTailThreads - 1];
+        __syncthreads();
+        uint32_t* tmp = cur;
+        cur = nxt;
+        nxt = tmp;
+        m = mNext;
+    }
+    if (t == 0) {   // the root, wherever the host expects the final clusters
+        cidA[0] = cur[0];
+        cidB[0] = cur[0];
+        misc[kMiscNodes] = sNodes;
+    }
 }
 
 __global__ void plocCompactKernel(const uint32_t* __restrict__ cid, const uint32_t* __restrict__ flag,
@@ -519,7 +605,8 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
         const uint32_t m0 = (uint32_t)n;
         WB_TRY(hipMemcpyAsync(misc + kMiscM, &m0, 4, hipMemcpyHostToDevice, st));
     }
-    for (int pass = 0; m > 1;) {
+    int pass = 0;
+    while (m > kTailMax) {
         if (pass > 4 * 64 + 64) {
             err = "wide BVH (device): clustering does not converge";
             return hipErrorUnknown;
@@ -549,6 +636,18 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
             return hipErrorUnknown;
         }
         m = mNext;
+    }
+    if (m > 1) {
+        uint32_t* a0 = static_cast<uint32_t*>(cid_[cur].p);
+        uint32_t* a1 = static_cast<uint32_t*>(cid_[cur ^ 1].p);
+        const uint32_t* mIn = misc + kMiscM + (pass & 1);
+        switch (radius) {
+            case 8: plocTailKernel<8><<<1, kTailThreads, 0, st>>>(a0, a1, pbox, pchild, nearest, flag, mIn, misc, (int)n, trav); break;
+            case 32: plocTailKernel<32><<<1, kTailThreads, 0, st>>>(a0, a1, pbox, pchild, nearest, flag, mIn, misc, (int)n, trav); break;
+            case 64: plocTailKernel<64><<<1, kTailThreads, 0, st>>>(a0, a1, pbox, pchild, nearest, flag, mIn, misc, (int)n, trav); break;
+            default: plocTailKernel<16><<<1, kTailThreads, 0, st>>>(a0, a1, pbox, pchild, nearest, flag, mIn, misc, (int)n, trav); break;
+        }
+        WB_TRY(hipGetLastError());
     }
     const uint32_t* rootCid = static_cast<const uint32_t*>(cid_[cur].p);
 
