@@ -193,8 +193,8 @@ int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int
  *   reference, not its random numbers; does not advance the film's XORWOW streams.  Needs
  *   chunk-count x pixels x 16 bytes of device memory for the block partials {sum xyz, rays}.
  *   The wide kernel builds its tree on the host at the first render after each
- *   pt_scene_build_bvh (C3 5,000 triangles ~25 ms, C5 1.04 M ~2 s); dynamic scenes that rebuild
- *   every frame may prefer PT_KERNEL_WAVEFRONT, whose tree is the device-built LBVH.
+ *   pt_scene_build_bvh (C3 5,000 triangles ~5 ms, C5 1.04 M ~0.8 s) unless the build was asked
+ *   for PT_BVH_WIDE_DEVICE (the tree built on the device, milliseconds: dynamic scenes).
  * leaf_batch / shade_batch: wavefront thresholds in lanes (0 = default).
  * flags: PT_RENDER_IDENTITY_ORDER disables the longest-tile-first launch order;
  *   PT_RENDER_ACCUMULATE adds the frame to the film's running sums (progressive rendering,
