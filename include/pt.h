@@ -131,7 +131,8 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n_objects,
  * same call (PLOC clustering + collapse, a few milliseconds even at a million primitives; for
  * dynamic scenes rebuilt every frame).  Without it PT_KERNEL_WIDE builds the tree at first use on
  * the host (binned SAH, slower to build; PT_WIDE_BUILD=device selects the device build there
- * too).  Either tree gives the same images. */
+ * too; after pt_scene_update_objects the device build is the default).  Either tree gives the
+ * same images. */
 #define PT_BVH_WIDE_DEVICE 4
 int pt_scene_build_bvh(pt_scene* scene, int flags);
 /* Dynamic scenes (per-frame rebuild): overwrite objects [first, first + n)
@@ -194,7 +195,9 @@ int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int
  *   chunk-count x pixels x 16 bytes of device memory for the block partials {sum xyz, rays}.
  *   The wide kernel builds its tree on the host at the first render after each
  *   pt_scene_build_bvh (C3 5,000 triangles ~5 ms, C5 1.04 M ~0.8 s) unless the build was asked
- *   for PT_BVH_WIDE_DEVICE (the tree built on the device, milliseconds: dynamic scenes).
+ *   for PT_BVH_WIDE_DEVICE (the tree built on the device, milliseconds), or on the device at
+ *   first use once the scene's objects have been updated (pt_scene_update_objects: a dynamic
+ *   scene; PT_WIDE_BUILD=host / device in the environment overrides).
  * leaf_batch / shade_batch: wavefront thresholds in lanes (0 = default).
  * flags: PT_RENDER_IDENTITY_ORDER disables the longest-tile-first launch order;
  *   PT_RENDER_ACCUMULATE adds the frame to the film's running sums (progressive rendering,

@@ -2039,6 +2039,7 @@ struct pt_scene {
     DevBuf wide, wprims, wshade, rankOf;    // compressed 8-wide tree, its primitive and shading records, leaf ranks (PT_KERNEL_WIDE)
     std::unique_ptr<pt::WideDevBuilder> wideDev;   // device build scratch (PT_BVH_WIDE_DEVICE), kept between builds
     bool wideReady = false;                 // the wide tree matches the current LBVH build
+    bool updated = false;                   // pt_scene_update_objects was called: a dynamic scene
     int wideSource = 0;                     // 1: host binned SAH, 2: device PLOC
     int wideDepth = 0;
     int64_t wideNodes = 0;                  // node slots
@@ -2341,6 +2342,7 @@ int pt_scene_update_objects(pt_scene* s, const pt_object* objs, int64_t first, i
     std::copy(objs, objs + n, s->objs.begin() + first);
     HIP_TRY(hipMemcpy(s->dobjs.as<pt_object>() + first, objs, (size_t)n * sizeof(pt_object), hipMemcpyHostToDevice));
     s->built = false;   // the hierarchy no longer matches the objects: rebuild before rendering
+    s->updated = true;  // from now on the wide tree is built on the device (once per rebuild)
     return PT_OK;
 }
 
@@ -2449,13 +2451,16 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
 }
 
 // The wide tree is only needed by PT_KERNEL_WIDE: unless pt_scene_build_bvh built it on the
-// device (PT_BVH_WIDE_DEVICE), built on first use after each LBVH build -- on the host (binned
-// SAH), or on the device when PT_WIDE_BUILD=device.
+// device (PT_BVH_WIDE_DEVICE), built on first use after each LBVH build -- on the device for a
+// scene whose objects were updated (dynamic: a rebuild per frame) or when PT_WIDE_BUILD=device,
+// else on the host (binned SAH: a few percent faster to trace, slower to build).
 static int ensureWide(pt_scene* s) {
     if (s->wideReady || s->nobj <= 0) return PT_OK;
     const auto t0 = std::chrono::steady_clock::now();
     const char* wb = std::getenv("PT_WIDE_BUILD");
-    int rc = (wb && std::string(wb) == "device") ? buildWideDevice(s, 0) : buildWide(s);
+    const std::string wbs = wb ? wb : "";
+    const bool device = wbs == "device" || (s->updated && wbs != "host");
+    int rc = device ? buildWideDevice(s, 0) : buildWide(s);
     if (!rc && s->wideSource == 2) HIP_TRY(hipStreamSynchronize(0));
     if (rc) return rc;
     s->wideReady = true;

@@ -201,3 +201,22 @@ def test_c5_wide_device_rebuild(pt, gpu):
     b, _ = pt.render(host, pt.Film(160, 90, seed=3), p.camera, 2, p.max_depth, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE)
     assert host.wide_info()["source"] == 1
     np.testing.assert_array_equal(bits(a), bits(b))
+
+
+def test_updated_scene_builds_wide_tree_on_device(pt, gpu, monkeypatch):
+    """A scene whose objects were updated is dynamic: without PT_BVH_WIDE_DEVICE its wide tree is
+    still built on the device at first use (a host SAH build per frame would dominate); a static
+    scene keeps the host tree.  The frames are the same either way."""
+    monkeypatch.delenv("PT_WIDE_BUILD", raising=False)
+    objs, mats = random_soup(400, 60, seed=61, spread=8.0)
+    cam = pt.camera_make((0, 2, 20), (0, 0, 0), 40.0, W / H)
+    static = pt.Scene(objs, mats, device=gpu)
+    a, _ = pt.render(static, pt.Film(W, H, seed=2), cam, 2, 8, kernel=pt.KERNEL_WIDE)
+    assert static.wide_info()["source"] == 1
+    dyn = pt.Scene(objs, mats, device=gpu)
+    dyn.update_objects(objs[:10])
+    dyn.build_bvh()
+    assert dyn.wide_info()["source"] == 0   # not built yet
+    b, _ = pt.render(dyn, pt.Film(W, H, seed=2), cam, 2, 8, kernel=pt.KERNEL_WIDE)
+    assert dyn.wide_info()["source"] == 2
+    np.testing.assert_array_equal(bits(a), bits(b))
