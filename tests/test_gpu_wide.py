@@ -178,3 +178,62 @@ def test_wide_large_soup_trace_and_render(pt, orc, gpu, wb):
         f = pt.Film(96, 64, 3, device=gpu)
         frames.append(pt.render(s, f, cam, 2, 12, kernel=k, rng=pt.RNG_SAMPLE, chunk=2)[0])
     np.testing.assert_array_equal(bits(frames[1]), bits(frames[0]))
+
+
+def edge_scene(kind):
+    """Scenes at the edges of the wide tree's encoding: tiny and huge coordinates (the plane
+    quantum is relative to the scene extent), degenerate triangles, everything at one point, a
+    huge ground sphere under small objects, very thin long triangles."""
+    rng = np.random.default_rng(76)
+    if kind == "tiny":
+        objs, mats = random_soup(800, 200, seed=71, spread=10.0)
+        objs["v"] *= np.float32(1e-3)
+        return objs, mats, 0.02
+    if kind == "huge":
+        objs, mats = random_soup(800, 200, seed=72, spread=10.0)
+        objs["v"] *= np.float32(1e4)
+        objs["v"] += np.float32(3e5)
+        return objs, mats, 2e5
+    if kind == "degenerate":
+        objs, mats = random_soup(600, 50, seed=73)
+        tri = np.flatnonzero(objs["type"] == 3)
+        objs["v"][tri[:200], 3:6] = objs["v"][tri[:200], 0:3]                 # zero-area: v1 == v0
+        objs["v"][tri[200:300], 6:9] = 2 * objs["v"][tri[200:300], 3:6] - objs["v"][tri[200:300], 0:3]  # collinear
+        return objs, mats, 15.0
+    if kind == "one_point":
+        objs, mats = random_soup(300, 100, seed=74, spread=0.0)
+        objs["v"][objs["type"] == 1, :3] = 0.0
+        return objs, mats, 5.0
+    if kind == "ground":
+        objs, mats = random_soup(500, 100, seed=75, spread=5.0)
+        g = objs[-1:].copy()
+        g["type"] = 1
+        g["v"][0, :4] = (0.0, -1000.0, 0.0, 1000.0)
+        return np.concatenate([objs, g]), mats, 20.0
+    if kind == "slivers":
+        n = 2000
+        objs = np.zeros(n, OBJECT_DTYPE)
+        objs["type"] = 3
+        a = rng.uniform(-10, 10, (n, 3)).astype(np.float32)
+        axis = rng.integers(0, 3, n)
+        b = a.copy()
+        b[np.arange(n), axis] += np.float32(40.0)
+        objs["v"][:, 0:3] = a
+        objs["v"][:, 3:6] = b
+        objs["v"][:, 6:9] = a + rng.uniform(-1e-3, 1e-3, (n, 3)).astype(np.float32)
+        mats = np.zeros(2, MATERIAL_DTYPE)
+        mats["type"] = 0
+        mats["albedo"] = 0.5
+        return objs, mats, 40.0
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["tiny", "huge", "degenerate", "one_point", "ground", "slivers"])
+def test_wide_edge_scenes(pt, orc, gpu, wb, kind):
+    objs, mats, radius = edge_scene(kind)
+    lo = objs["v"][:, :3].min(0)
+    hi = objs["v"][:, :3].max(0)
+    center = (lo + hi) / 2 if kind != "ground" else np.zeros(3)
+    rays = random_rays(4096, seed=80, center=center, radius=radius, objects=objs)
+    hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
+    assert_hits_equal(hits, ref)
