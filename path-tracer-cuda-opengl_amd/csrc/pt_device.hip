@@ -877,6 +877,31 @@ constexpr int kWavesPerEU = WIDE ? PT_WIDE_WAVES_PER_EU : kLdsStack<STACK, SAMPL
 // order, the nearest first), a primitive group (tgBase, tg = hit leaf primitives); NODE takes the
 // next child of the group (pushing the rest), LEAF tests up to two primitives, keeping the
 // minimum (t, tie rank) of wideTest -- the reference's closest hit, in any visiting order.
+// Kernel arguments re-read from the kernarg segment where a rare step needs them (one scalar
+// load) instead of being held in SGPRs across the step loop: the loop's uniform state exceeded
+// the SGPR budget and the compiler parked the overflow in VGPR lanes, paying a v_readlane -- a
+// VALU issue slot in an issue-bound kernel -- per use.  The empty asm hides the pointer's origin
+// so the loads are not hoisted out of the loop again.
+typedef const __attribute__((address_space(4))) RenderParams* KArgs;
+__device__ __forceinline__ KArgs kargs() {
+    KArgs k = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return k;
+}
+
+typedef const __attribute__((address_space(4))) float KFloat;
+__device__ __forceinline__ float3 ld3(const __attribute__((address_space(4))) float3& v) {
+    KFloat* f = (KFloat*)&v;
+    return f3(f[0], f[1], f[2]);
+}
+__device__ __forceinline__ DevScene ldScene(KArgs k) {
+    DevScene S;
+    S.nodes = k->S.nodes; S.prims = k->S.prims; S.shade = k->S.shade; S.mats = k->S.mats;
+    S.wnodes = k->S.wnodes; S.wprims = k->S.wprims; S.wshade = k->S.wshade; S.rankOf = k->S.rankOf;
+    S.iparent = k->S.iparent; S.err = k->S.err; S.nprims = k->S.nprims;
+    return S;
+}
+
 template <int STACK, bool SAMPLE, bool WIDE>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
     // Deep trees (binary kernels) keep 32 stack entries per lane in LDS (8 KB per wave: 5 waves
@@ -988,6 +1013,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // that received a task; lanes that find the counter exhausted stop asking.
 #define PT_TAKE_TASKS(got)                                                                          \
     do {                                                                                          \
+        const auto& Q_ = *kargs();                                                                \
         for (;;) {                                                                                \
             const uint64_t m_ = __ballot(needTask);                                               \
             if (m_ == 0) break;                                                                   \
@@ -997,7 +1023,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 /* always a full pool: = one (tile, block) group, one task per lane; smaller    \
                    grabs near the end measured slower (1/8 share: 150-158 vs 145 ms) */          \
                 const uint32_t grab_ = (uint32_t)kTaskPool;                                       \
-                if (lane == leader_) b_ = atomicAdd(P.taskCounter, grab_);                        \
+                if (lane == leader_) b_ = atomicAdd(Q_.taskCounter, grab_);                        \
                 poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
                 poolLeft = grab_;                                                                 \
             }                                                                                     \
@@ -1007,31 +1033,31 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             poolBase += take_;                                                                    \
             poolLeft -= take_;                                                                    \
             const uint32_t g0_ = base_ >> 6, off_ = base_ & 63u;                                  \
-            const uint32_t slotA_ = g0_ / (uint32_t)P.nblocks, blkA_ = g0_ - slotA_ * (uint32_t)P.nblocks; \
-            const bool wrap_ = blkA_ + 1u == (uint32_t)P.nblocks;                                  \
+            const uint32_t slotA_ = g0_ / (uint32_t)Q_.nblocks, blkA_ = g0_ - slotA_ * (uint32_t)Q_.nblocks; \
+            const bool wrap_ = blkA_ + 1u == (uint32_t)Q_.nblocks;                                  \
             const uint32_t slotB_ = wrap_ ? slotA_ + 1u : slotA_, blkB_ = wrap_ ? 0u : blkA_ + 1u; \
-            const uint32_t nslots_ = (uint32_t)P.ntiles;                                          \
-            const uint32_t tA_ = slotA_ < nslots_ ? (P.tileOrder ? (uint32_t)P.tileOrder[slotA_] : slotA_) : 0u; \
-            const uint32_t tB_ = slotB_ < nslots_ ? (P.tileOrder ? (uint32_t)P.tileOrder[slotB_] : slotB_) : 0u; \
-            const uint32_t tyA_ = tA_ / (uint32_t)P.tiles_x, txA_ = tA_ - tyA_ * (uint32_t)P.tiles_x; \
-            const uint32_t tyB_ = tB_ / (uint32_t)P.tiles_x, txB_ = tB_ - tyB_ * (uint32_t)P.tiles_x; \
+            const uint32_t nslots_ = (uint32_t)Q_.ntiles;                                          \
+            const uint32_t tA_ = slotA_ < nslots_ ? (Q_.tileOrder ? (uint32_t)Q_.tileOrder[slotA_] : slotA_) : 0u; \
+            const uint32_t tB_ = slotB_ < nslots_ ? (Q_.tileOrder ? (uint32_t)Q_.tileOrder[slotB_] : slotB_) : 0u; \
+            const uint32_t tyA_ = tA_ / (uint32_t)Q_.tiles_x, txA_ = tA_ - tyA_ * (uint32_t)Q_.tiles_x; \
+            const uint32_t tyB_ = tB_ / (uint32_t)Q_.tiles_x, txB_ = tB_ - tyB_ * (uint32_t)Q_.tiles_x; \
             const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));                 \
             if (needTask && k_ < take_) {                                                         \
-                if (base_ + k_ >= P.ntasks) {                                                     \
+                if (base_ + k_ >= Q_.ntasks) {                                                     \
                     needTask = false;                                                             \
                 } else {                                                                          \
                     const uint32_t o_ = off_ + k_, px_ = o_ & 63u;                                \
                     const bool hi_ = o_ >= 64u;                                                   \
                     const int c_ = (int)((hi_ ? txB_ : txA_) * 8u + (px_ & 7u));                  \
                     const int r_ = (int)((hi_ ? tyB_ : tyA_) * 8u + (px_ >> 3));                  \
-                    if (c_ < P.width && r_ < P.nrows) {                                           \
+                    if (c_ < Q_.width && r_ < Q_.nrows) {                                           \
                         needTask = false;                                                         \
                         got = true;                                                               \
                         taskRays = 0;                                                             \
                         cr = (uint32_t)c_ | ((uint32_t)r_ << 16);                                 \
-                        frow = (float)globalRow(r_, P.stripe_h, P.nparts, P.part);                \
-                        sample = (int)(hi_ ? blkB_ : blkA_) * P.block;                            \
-                        nSamples = min(sample + P.block, P.spp);                                  \
+                        frow = (float)globalRow(r_, Q_.stripe_h, Q_.nparts, Q_.part);                \
+                        sample = (int)(hi_ ? blkB_ : blkA_) * Q_.block;                            \
+                        nSamples = min(sample + Q_.block, Q_.spp);                                  \
                         sum = f3(0.0f, 0.0f, 0.0f);                                               \
                     }                                                                             \
                 }                                                                                 \
@@ -1041,10 +1067,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Sample mode: the lane's block is complete -> its sum, cost; ask for the next task.
 #define PT_FINISH_TASK()                                                                            \
     do {                                                                                          \
-        const uint32_t blk_ = (uint32_t)(nSamples - 1) / (uint32_t)P.block;                        \
+        const auto& Q_ = *kargs();                                                                \
+        const uint32_t blk_ = (uint32_t)(nSamples - 1) / (uint32_t)Q_.block;                        \
         const uint32_t c_ = cr & 0xffffu, r_ = cr >> 16;                                          \
-        float4* pp_ = reinterpret_cast<float4*>(P.partial) +                                      \
-                      ((size_t)blk_ * ((size_t)P.width * (size_t)P.nrows) + (size_t)(r_ * (uint32_t)P.width + c_)); \
+        float4* pp_ = reinterpret_cast<float4*>(Q_.partial) +                                      \
+                      ((size_t)blk_ * ((size_t)Q_.width * (size_t)Q_.nrows) + (size_t)(r_ * (uint32_t)Q_.width + c_)); \
         /* one 16-B store: the block sum and the task's ray count (the tile cost, summed by the \
            resolve pass; a per-task global atomic here cost 14 % of the frame) */              \
         *pp_ = make_float4(sum.x, sum.y, sum.z, __uint_as_float(taskRays + 1u));                  \
@@ -1052,18 +1079,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
+        const auto& Q_ = *kargs();                                                                \
         if constexpr (PARK && !SAMPLE) fcol = (float)(cr & 0xffffu);                              \
         if constexpr (SAMPLE) {                                                                   \
             fcol = (float)(cr & 0xffffu);                                                         \
-            g = sampleStream(P.seed0, P.seed1, P.sampleBase + (uint32_t)sample,                   \
-                             (uint32_t)frow * (uint32_t)P.width + (cr & 0xffffu));                \
+            g = sampleStream(Q_.seed0, Q_.seed1, Q_.sampleBase + (uint32_t)sample,                   \
+                             (uint32_t)frow * (uint32_t)Q_.width + (cr & 0xffffu));                \
         }                                                                                         \
-        const float u_ = (fcol + g.uniform()) * P.invW;                                           \
-        const float v_ = (frow + g.uniform()) * P.invH;                                           \
-        o = P.cam.pos;                                                                            \
-        d = sub(add(add(P.cam.ll, scale(u_, P.cam.hor)), scale(v_, P.cam.ver)), P.cam.pos);       \
+        const float u_ = (fcol + g.uniform()) * Q_.invW;                                           \
+        const float v_ = (frow + g.uniform()) * Q_.invH;                                           \
+        o = ld3(Q_.cam.pos);                                                                            \
+        d = sub(add(add(ld3(Q_.cam.ll), scale(u_, ld3(Q_.cam.hor))), scale(v_, ld3(Q_.cam.ver))), ld3(Q_.cam.pos));       \
         att = f3(1.0f, 1.0f, 1.0f);                                                               \
-        depthLeft = P.max_depth;                                                                  \
+        depthLeft = Q_.max_depth;                                                                  \
     } while (0)
 
     bool started = false;
@@ -1329,9 +1357,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 const bool redo = wantShade && !needTask && (oct & 8u);
                 PT_DIAG_ADD(sRedo, (uint32_t)__popcll(__ballot(redo)));
                 if (redo) {
+                    const DevScene S2 = ldScene(kargs());
                     closest = __builtin_inff();
-                    const int k = traceRefStackless(S, o, d, 0.001f, closest);
-                    best = k >= 0 ? (int)S.rankOf[k] : -1;
+                    const int k = traceRefStackless(S2, o, d, 0.001f, closest);
+                    best = k >= 0 ? (int)S2.rankOf[k] : -1;
                 }
             }
             PT_UNPARK();
@@ -1344,7 +1373,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     contrib = sky(d, att);
                     done = true;
                 } else {
-                    HitRec h = WIDE ? makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d) : makeHit(S, best, closest, o, d);
+                    HitRec h = WIDE ? makeHitFrom(kargs()->S.wshade, best & (int)kPrimMask, closest, o, d) : makeHit(S, best, closest, o, d);
                     float3 na;
                     if (!scatter(S, h, d, na, g)) {
                         done = true;
