@@ -1289,13 +1289,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (h0) { k0 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
                 const bool h1 = tg != 0u;
                 if (h1) { k1 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
-                Prim q0{}, q1{};
-                {
-                    const float4* w0 = S.wprims + 3 * (size_t)k0;
-                    const float4* w1 = S.wprims + 3 * (size_t)k1;
-                    if (h0) q0 = Prim{w0[0], w0[1], w0[2]};
-                    if (h1) q1 = Prim{w1[0], w1[1], w1[2]};
-                }
+                // Every lane loads two records (lanes without a primitive read record 0): a
+                // conditional load would cost a zero fill of 24 registers per step
+                const float4* w0 = S.wprims + 3 * (size_t)k0;
+                const float4* w1 = S.wprims + 3 * (size_t)k1;
+                const Prim q0{w0[0], w0[1], w0[2]}, q1{w1[0], w1[1], w1[2]};
                 bool redo = false;
                 if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                 if (h1) wideTest(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
