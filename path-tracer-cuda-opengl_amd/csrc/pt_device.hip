@@ -123,10 +123,12 @@ struct Xorwow {
 // Any sample of any pixel starts anywhere, in one block of work.
 __device__ __forceinline__ Xorwow sampleStream(uint32_t k0, uint32_t k1, uint32_t sample, uint32_t pixel) {
     uint32_t c0 = sample, c1 = pixel, c2 = 0u, c3 = 0x53414D50u;
-#pragma unroll 1   // (a rolled loop keeps register pressure at the camera-ray site low)
+#pragma unroll 2   // (pairs of rounds: no register moves; a full unroll raises the camera-ray site's pressure)
     for (int r = 0; r < 10; r++) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        // one 32 x 32 -> 64 multiply per word (v_mad_u64_u32) instead of mul_hi + mul_lo
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u;
