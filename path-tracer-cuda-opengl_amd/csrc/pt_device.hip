@@ -864,6 +864,9 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
                          // C3 @256 spp: 5 waves 172.4 ms, 6 waves 174.6 ms, not parked at 5 waves 166.8 ms)
 #endif
 constexpr int kParkWords = 18;
+#ifndef PT_WIDE_SPEC
+#define PT_WIDE_SPEC 1   // wide kernels: speculative traversal (lanes with primitives waiting keep visiting nodes)
+#endif
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
@@ -915,6 +918,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // traversal state alone in registers (6 waves per SIMD without spills).  park[w * 64 + lane].
     constexpr bool PARK = WIDE && PT_WIDE_PARK;
     __shared__ uint32_t park[PARK ? kParkWords * kWave : 1];
+    // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
+    // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
+    // marks it) and comes back when the current group is empty.
+    constexpr bool SPEC = WIDE && PT_WIDE_SPEC;
+    __shared__ uint32_t pend[SPEC ? 2 * kWave : 1];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -944,6 +952,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
 #ifdef PT_DIAG
     uint32_t itN = 0, itL = 0, itS = 0, sPops = 0, sRedo = 0;   // scheduler diagnostics (iterations per kind)
+    unsigned long long sSpecN = 0, sIdleN = 0;   // NODE steps: lanes waiting on primitives that have nodes left; lanes with no NODE work
     unsigned long long cycN = 0, cycL = 0, cycS = 0;   // and shader cycles per kind
     unsigned long long cycSh = 0, cycTk = 0, cycNp = 0, cycBr = 0;   // SHADE: shading, tasks, new path, ray start
 #define PT_DIAG_ADD(v, x) (v) += (x)
@@ -1168,7 +1177,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
-        const bool wantNode = WIDE ? (tg == 0u && ((ng & 0xffu) != 0u || sp > 0)) : (node >= 0 && qn <= LQ - 2);
+        const bool wantNode = WIDE ? ((SPEC ? (tg == 0u || !(oct & 16u)) : tg == 0u) && ((ng & 0xffu) != 0u || sp > 0))
+                                   : (node >= 0 && qn <= LQ - 2);
         const bool wantLeaf = WIDE ? tg != 0u : qn > 0;
         const bool wantShade = (active && (WIDE ? (tg == 0u && (ng & 0xffu) == 0u && sp == 0) : (node == -1 && qn == 0))) ||
                                needTask;
@@ -1190,7 +1200,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             sVisits += (uint32_t)nN;
             PT_DIAG_ADD(itN, 1u);
             if constexpr (WIDE) {
+                PT_DIAG_ADD(sSpecN, (unsigned long long)__popcll(__ballot(tg != 0u && ((ng & 0xffu) != 0u || sp > 0))));
+                PT_DIAG_ADD(sIdleN, (unsigned long long)(64 - nN));
+            }
+            if constexpr (WIDE) {
                 if (wantNode) {
+                    if (SPEC && tg != 0u) {   // park the waiting primitive group, keep traversing
+                        pend[lane] = tgBase;
+                        pend[kWave + lane] = tg;
+                        oct |= 16u;
+                    }
+                    // (the parked values are read back from LDS, not kept in registers meanwhile)
+                    if constexpr (SPEC) asm volatile("" ::: "memory");
                     if ((ng & 0xffu) == 0u) { sp--; ng = my[sp * kWave]; }   // the group below
                     const uint32_t bit = (uint32_t)__builtin_ctz(ng & 0xffu);   // nearest remaining child
                     const uint32_t child = (ng >> 8) + (bit ^ (oct & 7u));
@@ -1206,6 +1227,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     ng = (n1.x << 8) | (hits >> 24);
                     tgBase = n1.y;
                     tg = hits & 0xffffffu;
+                    if (SPEC && tg == 0u && (oct & 16u)) {   // no new primitives: the parked group is current again
+                        tgBase = pend[lane];
+                        tg = pend[kWave + lane];
+                        oct &= ~16u;
+                    }
                 }
             } else if (wantNode) {
 #if PT_NODE_BUFFER_LOADS
@@ -1300,6 +1326,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                 if (h1) wideTest(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                 if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
+                if (SPEC && tg == 0u && (oct & 16u)) {   // this group is done: the parked one is next
+                    tgBase = pend[lane];
+                    tg = pend[kWave + lane];
+                    oct &= ~16u;
+                }
                 const bool s0 = __float_as_uint(q0.p2.w) != 0u, s1 = __float_as_uint(q1.p2.w) != 0u;
                 sTris += (uint32_t)__popcll(__ballot(h0 && !s0)) + (uint32_t)__popcll(__ballot(h1 && !s1));
                 sSph += (uint32_t)__popcll(__ballot(h0 && s0)) + (uint32_t)__popcll(__ballot(h1 && s1));
@@ -1472,6 +1503,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         atomicAdd(P.counters + 18, cycNp);
         atomicAdd(P.counters + 19, cycBr);
         atomicAdd(P.counters + 20, (unsigned long long)sRedo);
+        atomicAdd(P.counters + 21, sSpecN);
+        atomicAdd(P.counters + 22, sIdleN);
 #endif
     }
 }
@@ -2940,7 +2973,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                      (double)c[14] / std::max(1ull, c[10]), (double)c[12] / (double)(c[12] + c[13] + c[14]),
                      (double)c[13] / (double)(c[12] + c[13] + c[14]), (double)c[14] / (double)(c[12] + c[13] + c[14]));
     if (std::getenv("PT_ITER_STATS") && kernel == PT_KERNEL_WIDE)
-        std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps)\n", c[20]);
+        std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps); NODE steps: "
+                     "lanes waiting on primitives with nodes left %.1f, lanes without NODE work %.1f\n", c[20],
+                     (double)c[21] / std::max(1ull, c[8]), (double)c[22] / std::max(1ull, c[8]));
     if (std::getenv("PT_ITER_STATS") && c[14] > 0)
         std::fprintf(stderr, "[pt] SHADE cycles/iteration: shading %.0f tasks %.0f new-path %.0f ray-start %.0f\n",
                      (double)c[16] / std::max(1ull, c[10]), (double)c[17] / std::max(1ull, c[10]),
