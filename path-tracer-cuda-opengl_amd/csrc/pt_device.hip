@@ -2426,7 +2426,7 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
         (rc = devReserve(s->nodes, ni * 4 * sizeof(float4))) || (rc = devReserve(s->keys, n1 * 8)) ||
         (rc = devReserve(s->leafBoxes, n1 * 24)) || (rc = devReserve(s->iparent, ni * 4)) ||
         (rc = devReserve(s->lparent, n1 * 4)) || (rc = devReserve(s->irange, ni * 8)) ||
-        (rc = devReserve(s->refitEvents, (ni + 1) * 4)))
+        (rc = devReserve(s->refitEvents, (n1 + 2) * 4)))   // count + at most (crossing nodes + 1) <= n arrivals
         return rc;
     DevBuf &codes = s->codes, &ids = s->ids, &codes2 = s->codes2, &ids2 = s->ids2, &box6 = s->box6, &sph = s->sph,
            &arr = s->arr, &dep = s->dep, &temp = s->sortTemp;
