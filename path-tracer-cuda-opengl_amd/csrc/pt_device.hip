@@ -673,6 +673,7 @@ struct RenderParams {
     uint32_t seed0, seed1;
     uint32_t sampleBase;                      // sample mode: index of the frame's first sample
     int rawOut;                               // compat: store the raw sample sum (resolveKernel follows)
+    int stripeShift, blockShift;              // log2(stripe_h), log2(block) when powers of two, else -1
 };
 
 // Compat mode end of a pixel: sqrt(sum / spp) (main.cu:290-293), or the raw sum when a resolve
@@ -688,6 +689,12 @@ __device__ __forceinline__ void storePixel(const RenderParams& P, size_t idx, fl
     }
 }
 
+// shift: log2(sh) when sh is a power of two, else -1 (shifts instead of two VALU divisions)
+__device__ __forceinline__ int globalRowFast(int lrow, int sh, int shift, int nparts, int part) {
+    if (nparts == 1) return lrow;
+    if (shift >= 0) return ((((lrow >> shift) * nparts + part)) << shift) + (lrow & (sh - 1));
+    return ((lrow / sh) * nparts + part) * sh + lrow % sh;
+}
 __device__ __forceinline__ int globalRow(int lrow, int sh, int nparts, int part) {
     return ((lrow / sh) * nparts + part) * sh + lrow % sh;
 }
@@ -1066,7 +1073,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                         got = true;                                                               \
                         taskRays = 0;                                                             \
                         cr = (uint32_t)c_ | ((uint32_t)r_ << 16);                                 \
-                        frow = (float)globalRow(r_, Q_.stripe_h, Q_.nparts, Q_.part);                \
+                        frow = (float)globalRowFast(r_, Q_.stripe_h, Q_.stripeShift, Q_.nparts, Q_.part); \
                         sample = (int)(hi_ ? blkB_ : blkA_) * Q_.block;                            \
                         nSamples = min(sample + Q_.block, Q_.spp);                                  \
                         sum = f3(0.0f, 0.0f, 0.0f);                                               \
@@ -1079,7 +1086,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #define PT_FINISH_TASK()                                                                            \
     do {                                                                                          \
         const auto& Q_ = *kargs();                                                                \
-        const uint32_t blk_ = (uint32_t)(nSamples - 1) / (uint32_t)Q_.block;                        \
+        const uint32_t blk_ = Q_.blockShift >= 0 ? (uint32_t)(nSamples - 1) >> Q_.blockShift            \
+                                                 : (uint32_t)(nSamples - 1) / (uint32_t)Q_.block;         \
         const uint32_t c_ = cr & 0xffffu, r_ = cr >> 16;                                          \
         float4* pp_ = reinterpret_cast<float4*>(Q_.partial) +                                      \
                       ((size_t)blk_ * ((size_t)Q_.width * (size_t)Q_.nrows) + (size_t)(r_ * (uint32_t)Q_.width + c_)); \
@@ -2789,6 +2797,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.width = f->width;
     P.nrows = f->nrows;
     P.stripe_h = f->stripe_h;
+    P.stripeShift = (f->stripe_h & (f->stripe_h - 1)) == 0 ? __builtin_ctz((unsigned)f->stripe_h) : -1;
     P.nparts = f->nparts;
     P.part = f->part;
     P.tiles_x = (f->width + 7) / 8;
@@ -2820,6 +2829,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.kernel = kernel;
     P.nblocks = 0;
     P.block = 0;
+    P.blockShift = -1;
     P.partial = nullptr;
     P.taskCounter = nullptr;
     P.stackSpill = nullptr;
@@ -2853,6 +2863,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
             return fail(PT_ERR_INVALID, "sample mode: frame width and rows must be < 65536");
         P.block = (opts && opts->chunk > 0) ? opts->chunk : std::max(16, (spp + 63) / 64);
         P.nblocks = (spp + P.block - 1) / P.block;
+        P.blockShift = (P.block & (P.block - 1)) == 0 ? __builtin_ctz((unsigned)P.block) : -1;
         const size_t need = (size_t)P.nblocks * (size_t)np * 16;   // {block sum xyz, rays}
         if (f->partialBytes < need) {
             if ((rc = devAlloc(f->partial, need))) return rc;
