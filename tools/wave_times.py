@@ -37,7 +37,12 @@ def main():
     name = {"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg]
     p = ptamd.Preset(name)
     scene = ptamd.Scene(p.objects, p.materials)
-    film = ptamd.Film(p.width, p.height, 1)
+    nparts = int(os.environ.get("NPARTS", "1"))   # one rank's share of an N-GPU frame
+    film = ptamd.Film(p.width, p.height, 1, stripe_height=8, n_parts=nparts, part=int(os.environ.get("PART", "0")))
+    if int(os.environ.get("WARM", "0")):   # one launch first: the next one runs longest-first
+        ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=ptamd.RNG_SAMPLE if os.environ.get("RNG") == "sample"
+                     else ptamd.RNG_COMPAT, chunk=int(os.environ.get("CHUNK", "0")))
+        film.reset()
     os.environ["PT_WAVE_TIMES"] = out
     rng = ptamd.RNG_SAMPLE if os.environ.get("RNG") == "sample" else ptamd.RNG_COMPAT
     rgb, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=int(os.environ.get("CHUNK", "0")))
