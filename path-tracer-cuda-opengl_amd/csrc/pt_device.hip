@@ -872,7 +872,7 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #endif
 constexpr int kParkWords = 18;
 #ifndef PT_WIDE_SPEC
-#define PT_WIDE_SPEC 1   // wide kernels: speculative traversal (lanes with primitives waiting keep visiting nodes)
+#define PT_WIDE_SPEC 1   // wide kernels: speculative traversal, primitive groups a lane may park while it keeps visiting nodes (0-3)
 #endif
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
@@ -928,8 +928,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
     // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
     // marks it) and comes back when the current group is empty.
-    constexpr bool SPEC = WIDE && PT_WIDE_SPEC;
-    __shared__ uint32_t pend[SPEC ? 2 * kWave : 1];
+    constexpr int SPECN = WIDE ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
+    constexpr bool SPEC = SPECN > 0;
+    __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1185,7 +1186,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
-        const bool wantNode = WIDE ? ((SPEC ? (tg == 0u || !(oct & 16u)) : tg == 0u) && ((ng & 0xffu) != 0u || sp > 0))
+        const bool wantNode = WIDE ? ((SPEC ? (tg == 0u || ((oct >> 4) & 3u) < (uint32_t)SPECN) : tg == 0u) &&
+                                      ((ng & 0xffu) != 0u || sp > 0))
                                    : (node >= 0 && qn <= LQ - 2);
         const bool wantLeaf = WIDE ? tg != 0u : qn > 0;
         const bool wantShade = (active && (WIDE ? (tg == 0u && (ng & 0xffu) == 0u && sp == 0) : (node == -1 && qn == 0))) ||
@@ -1214,9 +1216,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             if constexpr (WIDE) {
                 if (wantNode) {
                     if (SPEC && tg != 0u) {   // park the waiting primitive group, keep traversing
-                        pend[lane] = tgBase;
-                        pend[kWave + lane] = tg;
-                        oct |= 16u;
+                        const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
+                        pend[(2u * c) * kWave + lane] = tgBase;
+                        pend[(2u * c + 1u) * kWave + lane] = tg;
+                        oct += 16u;
                     }
                     // (the parked values are read back from LDS, not kept in registers meanwhile)
                     if constexpr (SPEC) asm volatile("" ::: "memory");
@@ -1235,10 +1238,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     ng = (n1.x << 8) | (hits >> 24);
                     tgBase = n1.y;
                     tg = hits & 0xffffffu;
-                    if (SPEC && tg == 0u && (oct & 16u)) {   // no new primitives: the parked group is current again
-                        tgBase = pend[lane];
-                        tg = pend[kWave + lane];
-                        oct &= ~16u;
+                    if (SPEC && tg == 0u && (oct & 48u)) {   // no new primitives: the last parked group is current again
+                        oct -= 16u;
+                        const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
+                        tgBase = pend[(2u * c) * kWave + lane];
+                        tg = pend[(2u * c + 1u) * kWave + lane];
                     }
                 }
             } else if (wantNode) {
@@ -1334,10 +1338,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                 if (h1) wideTest(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                 if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
-                if (SPEC && tg == 0u && (oct & 16u)) {   // this group is done: the parked one is next
-                    tgBase = pend[lane];
-                    tg = pend[kWave + lane];
-                    oct &= ~16u;
+                if (SPEC && tg == 0u && (oct & 48u)) {   // this group is done: the last parked one is next
+                    oct -= 16u;
+                    const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
+                    tgBase = pend[(2u * c) * kWave + lane];
+                    tg = pend[(2u * c + 1u) * kWave + lane];
                 }
                 const bool s0 = __float_as_uint(q0.p2.w) != 0u, s1 = __float_as_uint(q1.p2.w) != 0u;
                 sTris += (uint32_t)__popcll(__ballot(h0 && !s0)) + (uint32_t)__popcll(__ballot(h1 && !s1));
