@@ -634,6 +634,56 @@ __device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, floa
     return false;
 }
 
+// scatter() with the attenuation applied in place (att *= albedo for Lambertian and metal): the
+// dielectric's (1, 1, 1) is skipped, exactly (x * 1.0f == x for the finite attenuations of a
+// path), and no attenuation value has to live across the material switch.
+template <class G>
+__device__ __forceinline__ bool scatterInto(const HitRec& h, float3& d, float3& att, G& g) {
+    const float4 m0 = h.m0;
+    const int type = h.type;
+    if (type == PT_LAMBERTIAN) {
+        float3 dir = add(h.n, onUnitSphere(g));
+        if (fabsf(dir.x) < 1e-7f && fabsf(dir.y) < 1e-7f && fabsf(dir.z) < 1e-7f) dir = h.n;
+        d = dir;
+        att = mul(att, xyz(m0));
+        return true;
+    }
+    if (type == PT_METAL) {
+        float3 refl = reflect3(normalize3(d), h.n);
+        float3 fz = inUnitSphere(g);
+        d = add(refl, scale(m0.w, fz));
+        att = mul(att, xyz(m0));
+        return dot3(d, h.n) > 0.0f;
+    }
+    if (type == PT_DIELECTRIC) {
+        const float ir = h.ir;
+        float ratio = h.front ? (1.0f / ir) : ir;
+        float3 ud = normalize3(d);
+        float cos_t = fminf(dot3(neg(ud), h.n), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        bool cannot = ratio * sin_t > 1.0f;
+        bool refl = cannot;
+        if (!cannot) {   // reflectance (physical.h:20-25), pow(x,5) = ((x*x)*(x*x))*x
+            float r0 = (1.0f - ratio) / (1.0f + ratio);
+            r0 = r0 * r0;
+            float x = 1.0f - cos_t;
+            float x2 = x * x;
+            float rf = r0 + (1.0f - r0) * ((x2 * x2) * x);
+            refl = rf > g.uniform();
+        }
+        if (refl) {
+            d = reflect3(ud, h.n);
+        } else {   // refract (physical.h:14-19)
+            float ct = fminf(dot3(neg(ud), h.n), 1.0f);
+            float3 perp = scale(ratio, add(ud, scale(ct, h.n)));
+            float3 par = scale(-sqrtf(fabsf(1.0f - len2(perp))), h.n);
+            d = add(perp, par);
+        }
+        return true;
+    }
+    return false;
+}
+
 // Sky (main.cu:34-36) times attenuation.
 __device__ __forceinline__ float3 sky(float3 d, float3 att) {
     float3 ud = normalize3(d);
@@ -1418,11 +1468,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     done = true;
                 } else {
                     HitRec h = WIDE ? makeHitFrom(kargs()->S.wshade, best & (int)kPrimMask, closest, o, d) : makeHit(S, best, closest, o, d);
-                    float3 na;
-                    if (!scatter(S, h, d, na, g)) {
+                    if (!scatterInto(h, d, att, g)) {
                         done = true;
                     } else {
-                        att = mul(att, na);
                         o = h.p;
                         if (depthLeft == 0) { contrib = sky(d, att); done = true; }
                     }
