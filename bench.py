@@ -147,6 +147,8 @@ def main() -> None:
     spp = args.spp or CONFIG_SPP.get(args.config, preset.spp)
     w, h, depth = preset.width, preset.height, preset.max_depth
     scene = ptamd.Scene(preset.objects, preset.materials, device=local)
+    scene.build_bvh()   # again: the first build in a process also pays one-time module loading
+    scene_build = {"lbvh_device_ms": scene.build_ms}
     film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
     max_rows = ptdist.max_rows(h, STRIPE, world)
     rgba8 = args.output == "rgba8"
@@ -185,6 +187,8 @@ def main() -> None:
     ref_st = frame(ptamd.KERNEL_SIMPLE)
     for _ in range(max(0, args.warmup - 1)):
         frame()
+    if args.kernel == "wide":   # the wide tree was built at the first wide render (host binned SAH)
+        scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -300,6 +304,13 @@ def main() -> None:
         }
         if compat:
             out["compat_mode"] = compat
+        if world == 1:   # the per-frame rebuild of a dynamic scene: LBVH + wide tree, both on the device
+            dyn = ptamd.Scene(preset.objects, preset.materials, device=local,
+                              flags=ptamd.PT_BVH_ORIGIN_BOUNDS | ptamd.PT_BVH_WIDE_DEVICE)
+            dyn.build_bvh(ptamd.PT_BVH_ORIGIN_BOUNDS | ptamd.PT_BVH_WIDE_DEVICE)   # a rebuild: buffers reused
+            scene_build["lbvh_plus_wide_tree_device_ms"] = dyn.build_ms
+            del dyn
+        out["scene_build"] = scene_build
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(preset)
         print(json.dumps(out), flush=True)
