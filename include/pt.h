@@ -159,6 +159,10 @@ int pt_trace_closest(pt_scene* scene, const pt_ray* rays, int64_t n, float tmin,
  * (see pt_render_ex); any other value the binary LBVH in the reference's order.  Same hits. */
 int pt_trace_closest_ex(pt_scene* scene, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel,
                         pt_hit* hits, pt_stats* stats);
+/* pt_trace_closest_ex on device-resident arrays (e.g. torch tensors): rays / hits are device
+ * pointers, traced on `stream` (a hipStream_t, may be NULL); returns when the batch is done. */
+int pt_trace_closest_device(pt_scene* scene, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel,
+                            pt_hit* hits, void* stream, pt_stats* stats);
 /* Per-pixel XORWOW streams, initRandom (main.cu:262-269): curand_init(seed, pixel, 0, ...)
  * for every pixel of the rows this film owns.  Rows are grouped in stripes of stripe_height;
  * stripe s belongs to part (s % n_parts).  n_parts = 1 owns the whole frame. */

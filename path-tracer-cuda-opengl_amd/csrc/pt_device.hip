@@ -1644,8 +1644,11 @@ __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* r
                                                      float tmax, pt_hit* hits, unsigned long long* counters) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * kWave + lane;
     Counters c{0, 0, 0, 0};
+    // grid-stride over the batch: the counters are summed once per wave at the end (one global
+    // atomic per counter per wave of a 64-ray block was the bottleneck of large batches)
+    for (int64_t base = (int64_t)blockIdx.x * kWave; base < n; base += (int64_t)gridDim.x * kWave) {
+    const int64_t i = base + lane;
     if (i < n) {
         const pt_ray r = rays[i];
         const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
@@ -1667,6 +1670,7 @@ __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* r
         }
         hits[i] = h;
     }
+    }
     waveReduceAdd(counters + 0, c.rays);
     waveReduceAdd(counters + 1, c.visits);
     waveReduceAdd(counters + 2, c.tris);
@@ -1680,10 +1684,11 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                                                          float tmax, pt_hit* hits, unsigned long long* counters) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * kWave + lane;
     uint32_t* my = stk + lane;
     const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(S.wnodes);
     Counters c{0, 0, 0, 0};
+    for (int64_t base = (int64_t)blockIdx.x * kWave; base < n; base += (int64_t)gridDim.x * kWave) {   // grid-stride
+    const int64_t i = base + lane;
     if (i < n) {
         const pt_ray r = rays[i];
         const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
@@ -1749,6 +1754,7 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
             hr.n[0] = x.n.x; hr.n[1] = x.n.y; hr.n[2] = x.n.z;
         }
         hits[i] = hr;
+    }
     }
     waveReduceAdd(counters + 0, c.rays);
     waveReduceAdd(counters + 1, c.visits);
@@ -2333,7 +2339,11 @@ int dispatchRender(int stack, const RenderParams& P, hipStream_t st) {
 }
 int dispatchTrace(int stack, bool wide, const DevScene& S, const pt_ray* r, int64_t n, float tmin, float tmax,
                   pt_hit* h, unsigned long long* cnt, hipStream_t st) {
-    const unsigned blocks = (unsigned)((n + kWave - 1) / kWave);
+    // a grid of at most 32 one-wave blocks per CU, striding over the batch
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + kWave - 1) / kWave, (int64_t)cus * 32);
     if (wide) {
         switch (stack) {
             case 8: traceKernelWide<8><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
@@ -2674,44 +2684,65 @@ int pt_trace_closest(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, flo
     return pt_trace_closest_ex(s, rays, n, tmin, tmax, PT_KERNEL_DEFAULT, hits, stats);
 }
 
-int pt_trace_closest_ex(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel, pt_hit* hits,
-                        pt_stats* stats) {
-    if (!s || n < 0 || (n > 0 && (!rays || !hits))) return fail(PT_ERR_INVALID, "pt_trace_closest: bad argument");
+}  // extern "C"
+
+namespace {
+// Closest hits of n rays: rays / hits are device arrays (dr, dh), traced on `st`; the host waits
+// for the end (counters and the guard word are read back).
+int traceDevice(pt_scene* s, const pt_ray* dr, int64_t n, float tmin, float tmax, int kernel, pt_hit* dh,
+                hipStream_t st, pt_stats* stats) {
     if (kernel != PT_KERNEL_DEFAULT && kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT &&
         kernel != PT_KERNEL_WIDE)
-        return fail(PT_ERR_INVALID, "pt_trace_closest_ex: unknown kernel");
+        return fail(PT_ERR_INVALID, "pt_trace_closest: unknown kernel");
     if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
     int rc = setDevice(s->device);
     if (rc) return rc;
     const bool wide = kernel == PT_KERNEL_WIDE;
     if (wide && (rc = ensureWide(s))) return rc;
     const int stack = wide ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
-    DevBuf dr, dh;
-    if ((rc = devAlloc(dr, n * sizeof(pt_ray))) || (rc = devAlloc(dh, n * sizeof(pt_hit)))) return rc;
-    if (n > 0) HIP_TRY(hipMemcpy(dr.p, rays, n * sizeof(pt_ray), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(s->counters.p, 0, kNumCounters * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(s->counters.p, 0, kNumCounters * sizeof(unsigned long long), st));
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, 0));
-    if (n > 0 && (rc = dispatchTrace(stack, wide, devScene(s), dr.as<pt_ray>(), n, tmin, tmax, dh.as<pt_hit>(),
-                                     s->counters.as<unsigned long long>(), 0))) {
+    HIP_TRY(hipEventRecord(e0, st));
+    if (n > 0 && (rc = dispatchTrace(stack, wide, devScene(s), dr, n, tmin, tmax, dh, s->counters.as<unsigned long long>(), st))) {
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
         return rc;
     }
-    HIP_TRY(hipEventRecord(e1, 0));
+    HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    if (n > 0) HIP_TRY(hipMemcpy(hits, dh.p, n * sizeof(pt_hit), hipMemcpyDeviceToHost));
     unsigned long long c[kNumCounters] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     c[4] = 0;
     fillStats(stats, c, ms, wide);
     if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
     return PT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int pt_trace_closest_ex(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel, pt_hit* hits,
+                        pt_stats* stats) {
+    if (!s || n < 0 || (n > 0 && (!rays || !hits))) return fail(PT_ERR_INVALID, "pt_trace_closest: bad argument");
+    int rc = setDevice(s->device);
+    if (rc) return rc;
+    DevBuf dr, dh;
+    if ((rc = devAlloc(dr, n * sizeof(pt_ray))) || (rc = devAlloc(dh, n * sizeof(pt_hit)))) return rc;
+    if (n > 0) HIP_TRY(hipMemcpy(dr.p, rays, n * sizeof(pt_ray), hipMemcpyHostToDevice));
+    if ((rc = traceDevice(s, dr.as<pt_ray>(), n, tmin, tmax, kernel, dh.as<pt_hit>(), 0, stats))) return rc;
+    if (n > 0) HIP_TRY(hipMemcpy(hits, dh.p, n * sizeof(pt_hit), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_trace_closest_device(pt_scene* s, const pt_ray* rays, int64_t n, float tmin, float tmax, int kernel,
+                            pt_hit* hits, void* stream, pt_stats* stats) {
+    if (!s || n < 0 || (n > 0 && (!rays || !hits))) return fail(PT_ERR_INVALID, "pt_trace_closest_device: bad argument");
+    return traceDevice(s, rays, n, tmin, tmax, kernel, hits, static_cast<hipStream_t>(stream), stats);
 }
 
 int pt_film_create(int device, int width, int height, int sh, int nparts, int part, uint64_t seed, pt_film** out) {

@@ -77,7 +77,7 @@ EXPORTS = [
     "pt_trace_closest", "pt_film_create", "pt_film_info", "pt_film_rows", "pt_film_get_rng", "pt_film_set_rng",
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
     "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
-    "pt_scene_update_objects", "pt_trace_closest_ex", "pt_scene_wide_info",
+    "pt_scene_update_objects", "pt_trace_closest_ex", "pt_scene_wide_info", "pt_trace_closest_device",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -109,6 +109,8 @@ _sig = {
                                      C.POINTER(C.c_int)]),
     "pt_trace_closest": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, _P, C.POINTER(Stats)]),
     "pt_trace_closest_ex": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, C.c_int, _P, C.POINTER(Stats)]),
+    "pt_trace_closest_device": (C.c_int, [_P, _P, C.c_int64, C.c_float, C.c_float, C.c_int, _P, _P,
+                                          C.POINTER(Stats)]),
     "pt_film_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                  C.POINTER(C.c_void_p)]),
     "pt_film_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64)]),
@@ -288,6 +290,15 @@ class Scene:
         _check(lib.pt_trace_closest_ex(self.h, _ptr(rays) if len(rays) else None, len(rays), tmin, tmax, kernel,
                                        _ptr(hits) if len(hits) else None, C.byref(st)), "pt_trace_closest_ex")
         return hits, st
+
+    def trace_device(self, rays_ptr: int, n: int, hits_ptr: int, tmin: float = 0.001, tmax: float = float("inf"),
+                     kernel: int = KERNEL_DEFAULT, stream=None):
+        """pt_trace_closest_device: rays_ptr / hits_ptr are device pointers to n RAY_DTYPE / HIT_DTYPE
+        records (e.g. torch uint8 tensors' data_ptr()); returns the stats."""
+        st = Stats()
+        _check(lib.pt_trace_closest_device(self.h, rays_ptr or None, n, tmin, tmax, kernel, hits_ptr or None,
+                                           stream, C.byref(st)), "pt_trace_closest_device")
+        return st
 
     def close(self) -> None:
         if self.h:

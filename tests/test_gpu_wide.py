@@ -9,6 +9,7 @@ device by pt_scene_build_bvh (PLOC + collapse, PT_BVH_WIDE_DEVICE).
 """
 import numpy as np
 import pytest
+import torch  # before libpt.so loads (the two must share torch's HIP runtime)
 
 from helpers import OBJECT_DTYPE, MATERIAL_DTYPE, deep_stack_scene, random_rays, random_soup, rays_to_struct
 
@@ -237,3 +238,21 @@ def test_wide_edge_scenes(pt, orc, gpu, wb, kind):
     rays = random_rays(4096, seed=80, center=center, radius=radius, objects=objs)
     hits, _, ref, _ = trace_both(pt, orc, gpu, wb, objs, mats, rays)
     assert_hits_equal(hits, ref)
+
+
+def test_trace_device_pointers_match_host_api(pt, orc, gpu, wb):
+    """pt_trace_closest_device on torch-owned device memory gives the host API's hit records, for
+    both trees and the binary kernel."""
+    objs, mats = random_soup(2000, 300, seed=91)
+    rays = rays_to_struct(random_rays(5000, seed=92, objects=objs), pt.RAY_DTYPE)
+    s = make_scene(pt, objs, mats, gpu, wb)
+    dev = torch.device("cuda", gpu)
+    rd = torch.from_numpy(rays.view(np.uint8).copy()).to(dev)
+    for k in (pt.KERNEL_WIDE, pt.KERNEL_WAVEFRONT):
+        want, wst = s.trace(rays, 0.001, np.inf, kernel=k)
+        hd = torch.zeros(len(rays) * pt.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        st = s.trace_device(rd.data_ptr(), len(rays), hd.data_ptr(), 0.001, np.inf, kernel=k,
+                            stream=torch.cuda.current_stream(dev).cuda_stream)
+        got = hd.cpu().numpy().view(pt.HIT_DTYPE)
+        assert_hits_equal(got, want)
+        assert (st.rays, st.node_visits, st.tri_tests) == (wst.rays, wst.node_visits, wst.tri_tests)
