@@ -32,6 +32,7 @@
 #include "../host/pt_wide8.hpp"
 #include "../host/pt_wide_dev.hpp"
 #include "pt.h"
+#include "pt_math.hpp"
 
 using pt::fail;
 
@@ -95,7 +96,7 @@ __device__ __forceinline__ float3 cross3(float3 u, float3 v) {
     return f3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 __device__ __forceinline__ float len2(float3 v) { return v.x * v.x + v.y * v.y + v.z * v.z; }
-__device__ __forceinline__ float3 divs(float3 v, float t) { return scale(1.0f / t, v); }
+__device__ __forceinline__ float3 divs(float3 v, float t) { return scale(rcpRN(t), v); }
 __device__ __forceinline__ float3 normalize3(float3 v) {
     float l = sqrtf(len2(v));
     if (l == 0.0f) return f3(0.0f, 0.0f, 0.0f);
@@ -258,7 +259,7 @@ __device__ __forceinline__ float primHitT(const Prim& q, bool sphere, float3 o, 
     if (det == 0.0f) return -1.0f;
     float3 s = sub(o, v0);
     float3 s2 = cross3(s, e1);
-    float inv = 1.0f / det;
+    float inv = rcpRN(det);
     float t = dot3(s2, e2) * inv;
     float b1 = dot3(s1, s) * inv;
     float b2 = dot3(s2, d) * inv;
@@ -317,7 +318,7 @@ __device__ __forceinline__ float primHitAny(const Prim& q, bool sphere, float3 o
     if (det == 0.0f) return -1.0f;
     float3 s = sub(o, v0);
     float3 s2 = cross3(s, e1);
-    float inv = 1.0f / det;
+    float inv = rcpRN(det);
     float t = dot3(s2, e2) * inv;
     float b1 = dot3(s1, s) * inv;
     float b2 = dot3(s2, d) * inv;
@@ -444,7 +445,7 @@ __device__ __forceinline__ int trace(const DevScene& S, float3 o, float3 d, floa
         primTest(S, ref, o, d, tmin, closest, best, c);
         return best;
     }
-    const float3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float3 inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
     int node = 0, sp = 0, guard = 0;
     for (;;) {
         // Each internal node is visited at most once per query; more means a corrupt tree.
@@ -485,7 +486,7 @@ __device__ __forceinline__ int traceRefStackless(const DevScene& S, float3 o, fl
         if (t1 >= 0.0f) { closest = t1; best = 0; }
         return best;
     }
-    const float3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float3 inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
     int node = 0, from = -1;   // from >= 0: returning from that child of `node`
     for (int guard = 0; guard <= 2 * S.nprims; guard++) {
         const float4* np = S.nodes + 4 * (size_t)node;
@@ -607,7 +608,7 @@ __device__ __forceinline__ bool scatter(const DevScene& S, const HitRec& h, floa
     if (type == PT_DIELECTRIC) {
         atten = f3(1.0f, 1.0f, 1.0f);
         const float ir = h.ir;
-        float ratio = h.front ? (1.0f / ir) : ir;
+        float ratio = h.front ? rcpRN(ir) : ir;
         float3 ud = normalize3(d);
         float cos_t = fminf(dot3(neg(ud), h.n), 1.0f);
         float sin_t = sqrtf(1.0f - cos_t * cos_t);
@@ -657,7 +658,7 @@ __device__ __forceinline__ bool scatterInto(const HitRec& h, float3& d, float3& 
     }
     if (type == PT_DIELECTRIC) {
         const float ir = h.ir;
-        float ratio = h.front ? (1.0f / ir) : ir;
+        float ratio = h.front ? rcpRN(ir) : ir;
         float3 ud = normalize3(d);
         float cos_t = fminf(dot3(neg(ud), h.n), 1.0f);
         float sin_t = sqrtf(1.0f - cos_t * cos_t);
@@ -1056,7 +1057,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         sp = 0;                                                                                   \
         qn = 0;                                                                                   \
         if constexpr (WIDE) {   /* the root is slot 0 of a virtual node at base 0 */              \
-            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
+            inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                         \
             oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);  \
             tg = 0u;                                                                              \
             bestLo = -__builtin_inff();                                                           \
@@ -1069,7 +1070,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (t1 >= 0.0f) { closest = t1; best = 0; }                                       \
             }                                                                                     \
         } else {                                                                                  \
-            inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);                                         \
+            inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                         \
             node = 0;                                                                             \
         }                                                                                         \
     } while (0)
@@ -1692,7 +1693,7 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
     if (i < n) {
         const pt_ray r = rays[i];
         const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
-        const float3 inv = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        const float3 inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
         const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
         float closest = tmax;
         int best = -1, sp = 0;

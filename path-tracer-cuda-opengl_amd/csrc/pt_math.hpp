@@ -1,0 +1,43 @@
+// Exact fp32 helpers shared by the render kernels (pt_device.hip) and their exhaustive checker
+// (tools/micro/rcp_check.hip).  Compiled with the kernels' flags: -ffp-contract=off, no fast math,
+// fp32 denormals on (HIP's default for gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+// The IEEE division 1.0f / x costs eleven VALU operations on gfx950 (v_div_scale x2, v_rcp_f32,
+// five FMAs / multiplies, v_div_fmas, v_div_fixup).  The reference divides by the determinant
+// of every triangle test (triangle.h / cuda_object.h:73-78), by every ray direction component
+// (aabb.h:24) and by every vector it normalises (vec3.h:89-91), so the render kernel spends a
+// measurable share of its issue slots there.
+//
+// rcpNewton: v_rcp_f32 (1 ulp) refined by one Newton step with fused multiply-adds,
+//   e = 1 - x * r,  y = r + e * r,
+// three VALU operations.  It equals 1.0f / x bit for bit for every x whose biased exponent lies
+// in [kRcpExpLo, kRcpExpHi]; tools/micro/rcp_check.hip compares the two over all 2^32 inputs on
+// the GPU (tests/test_gpu_math.py) and reports the exponents where they differ (zeros,
+// denormals, and magnitudes whose reciprocal is denormal).  rcpRN takes the division for those.
+constexpr uint32_t kRcpExpLo = 1u;     // smallest biased exponent of the fast path
+constexpr uint32_t kRcpExpHi = 252u;   // largest (|x| < 2^126: the reciprocal is a normal number)
+
+__device__ __forceinline__ float rcpNewton(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+
+#ifndef PT_FAST_RCP
+#define PT_FAST_RCP 1   // 0: every reciprocal is the IEEE division (A/B builds)
+#endif
+
+__device__ __forceinline__ float rcpRN(float x) {
+    if constexpr (!PT_FAST_RCP) return 1.0f / x;
+    const uint32_t ex = (__float_as_uint(x) >> 23) & 0xffu;
+    float y;
+    if (__builtin_expect(ex - kRcpExpLo > kRcpExpHi - kRcpExpLo, 0)) {
+        y = 1.0f / x;   // zero, denormal, huge, inf, NaN: the IEEE division
+    } else {
+        y = rcpNewton(x);
+    }
+    return y;
+}

@@ -1,0 +1,29 @@
+"""The render kernels' reciprocal (csrc/pt_math.hpp: v_rcp_f32 + one fused Newton step, the IEEE
+division outside the checked exponent range) equals the IEEE division 1.0f / x for all 2^32 fp32
+inputs, on the GPU (tools/micro/rcp_check.hip, built by the package Makefile with the kernels'
+flags).  Tolerance: 0 ulp -- every triangle test, ray setup and normalisation of the reference
+(triangle determinant, aabb.h:24, vec3.h:89-91) goes through it, and the frames stay bit-exact
+against the oracle (test_gpu_parity.py)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHECK = os.path.join(REPO, "tools", "micro", "rcp_check")
+
+
+@pytest.mark.gpu
+def test_fast_reciprocal_equals_ieee_division_for_every_input():
+    assert os.path.exists(CHECK), "tools/micro/rcp_check not built (make -C path-tracer-cuda-opengl_amd)"
+    out = subprocess.run([CHECK], capture_output=True, text=True, timeout=120)
+    assert out.returncode in (0, 1), out.stderr
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["inputs"] == 2 ** 32
+    assert res["rcpRN_mismatches"] == 0
+    assert res["newton_mismatches_in_fast_range"] == 0
+    # the bare Newton step differs only for zeros / denormals and |x| >= 2^126 (denormal results)
+    lo, hi = res["fast_range"]
+    assert all(not (lo <= int(e) <= hi) for e in res["newton_mismatches_by_exponent"])
+    assert out.returncode == 0

@@ -1,5 +1,6 @@
 """Render one frame (profiling target).  usage: python tools/one_frame.py [c2|c3|c5] [spp] [compat|sample] [chunk]
 REPEAT=n renders n frames (later launches use the measured tile costs) and reports the fastest."""
+import hashlib
 import json
 import os
 import sys
@@ -18,11 +19,13 @@ p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[c
 scene = ptamd.Scene(p.objects, p.materials)
 film = ptamd.Film(p.width, p.height, 1)
 best = None
+digest = None
 for _ in range(int(os.environ.get("REPEAT", "1"))):   # later launches use measured tile costs
     film.reset()
-    _, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=chunk)
+    img, st = ptamd.render(scene, film, p.camera, spp, p.max_depth, rng=rng, chunk=chunk)
+    digest = hashlib.sha1(img.tobytes()).hexdigest()[:16]   # same for every library build that renders the same frame
     if best is None or st.kernel_ms < best.kernel_ms:
         best = st
 st = best
 print(json.dumps({"cfg": cfg, "spp": spp, "kernel_ms": st.kernel_ms, "rays": st.rays, "node_visits": st.node_visits,
-                  "tri_tests": st.tri_tests}))
+                  "tri_tests": st.tri_tests, "image": digest}))
