@@ -114,8 +114,10 @@ struct Xorwow {
         d += 362437u;
         return v4 + d;
     }
-    // curand_uniform: x * 2^-32 + 2^-33 in (0, 1]
-    __device__ __forceinline__ float uniform() { return (float)next() * 0x1p-32f + 0x1p-33f; }
+    // curand_uniform: x * 2^-32 + 2^-33 in (0, 1] (one exact FMA, pt_math.hpp)
+    __device__ __forceinline__ float uniform() { return uniformOf(next()); }
+    // 2 * (uniform() - 0.5f): the unit-sphere coordinates (one exact FMA, pt_math.hpp)
+    __device__ __forceinline__ float centered2() { return centered2Of(uniform()); }
 };
 
 // Sample mode stream of (pixel p, sample s): one Philox4x32-10 block (Salmon et al. 2011)
@@ -563,11 +565,11 @@ template <class G>
 __device__ __forceinline__ float3 onUnitSphere(G& g) {
     float3 res;
     float norm;
-    do {
-        float a = g.uniform() - 0.5f;
-        float b = g.uniform() - 0.5f;
-        float cz = g.uniform() - 0.5f;
-        res = scale(2.0f, f3(a, b, cz));
+    do {   // draws x, y, z in order; centered2() = 2 * (uniform() - 0.5f) exactly
+        const float a = g.centered2();
+        const float b = g.centered2();
+        const float cz = g.centered2();
+        res = f3(a, b, cz);
         norm = len2(res);
     } while (norm >= 1.0f);
     return divs(res, sqrtf(norm));
@@ -576,10 +578,10 @@ template <class G>
 __device__ __forceinline__ float3 inUnitSphere(G& g) {
     float3 res;
     do {
-        float a = g.uniform() - 0.5f;
-        float b = g.uniform() - 0.5f;
-        float cz = g.uniform() - 0.5f;
-        res = scale(2.0f, f3(a, b, cz));
+        const float a = g.centered2();
+        const float b = g.centered2();
+        const float cz = g.centered2();
+        res = f3(a, b, cz);
     } while (len2(res) >= 1.0f);
     return res;
 }
@@ -1590,7 +1592,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 // blocks are added to its tile's cost (the next launch's longest-first order).
 __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ src, int nblocks, float* accum,
                                                      float inv, int format, void* out, int64_t npix,
-                                                     unsigned* tileCost, int width, int tilesX) {
+                                                     unsigned* tileCost, int width, int tilesX, int costMax) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix) return;
     float x, y, z;
@@ -1609,7 +1611,9 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
         }
         if (tileCost) {
             const int row = (int)(i / width), col = (int)(i - (int64_t)row * width);
-            atomicAdd(tileCost + (row >> 3) * tilesX + (col >> 3), rays);
+            unsigned* tc = tileCost + (row >> 3) * tilesX + (col >> 3);
+            if (costMax) atomicMax(tc, rays);
+            else atomicAdd(tc, rays);
         }
     }
     if (accum) {
@@ -3029,7 +3033,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                                                                      accumulate ? f->accum.as<float>() : nullptr,
                                                                      inv, fmt, dst, np,
                                                                      sample ? f->tileCost.as<unsigned>() : nullptr,
-                                                                     f->width, P.tiles_x);
+                                                                     f->width, P.tiles_x, envInt("PT_TILE_KEY_MAX", 1));
         HIP_TRY(hipGetLastError());
     }
     if (accumulate) f->accumSamples += spp;

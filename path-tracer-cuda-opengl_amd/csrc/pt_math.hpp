@@ -41,3 +41,14 @@ __device__ __forceinline__ float rcpRN(float x) {
     }
     return y;
 }
+
+// curand_uniform (x * 2^-32 + 2^-33, in (0, 1]) as one FMA: (float)x is 0 or >= 1, so its product
+// with 2^-32 is exact and normal, and fma rounds the same exact sum the separate multiply and
+// add round.  Checked against the two-operation form for all 2^32 x (tools/micro/rcp_check.hip).
+__device__ __forceinline__ float uniformOf(uint32_t x) { return __builtin_fmaf((float)x, 0x1p-32f, 0x1p-33f); }
+
+// The coordinates of random_in_unit_sphere / random_unit_vector (utility.h:51-62, 73-82):
+// 2 * (u - 0.5f).  Doubling is exact and commutes with rounding for normal values and zero, so
+// round(2u - 1) = 2 * round(u - 0.5): one FMA instead of a subtract and a multiply.  Checked for
+// every u = uniformOf(x) (tools/micro/rcp_check.hip).
+__device__ __forceinline__ float centered2Of(float u) { return __builtin_fmaf(u, 2.0f, -1.0f); }

@@ -3,7 +3,9 @@ division outside the checked exponent range) equals the IEEE division 1.0f / x f
 inputs, on the GPU (tools/micro/rcp_check.hip, built by the package Makefile with the kernels'
 flags).  Tolerance: 0 ulp -- every triangle test, ray setup and normalisation of the reference
 (triangle determinant, aabb.h:24, vec3.h:89-91) goes through it, and the frames stay bit-exact
-against the oracle (test_gpu_parity.py)."""
+against the oracle (test_gpu_parity.py).  The same run checks the XORWOW draw mappings
+(curand_uniform and the unit-sphere coordinates 2 * (u - 0.5f), each one FMA) against their
+separately rounded forms for all 2^32 draws."""
 import json
 import os
 import subprocess
@@ -26,4 +28,7 @@ def test_fast_reciprocal_equals_ieee_division_for_every_input():
     # the bare Newton step differs only for zeros / denormals and |x| >= 2^126 (denormal results)
     lo, hi = res["fast_range"]
     assert all(not (lo <= int(e) <= hi) for e in res["newton_mismatches_by_exponent"])
+    # the draw mappings: uniformOf (one FMA) == x * 2^-32 + 2^-33, centered2Of == (u - 0.5f) * 2
+    assert res["uniform_fma_mismatches"] == 0
+    assert res["centered2_fma_mismatches"] == 0
     assert out.returncode == 0

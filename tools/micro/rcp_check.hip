@@ -1,5 +1,6 @@
 // Exhaustive check of the render kernels' reciprocal (csrc/pt_math.hpp) against the IEEE
-// division 1.0f / x over all 2^32 fp32 bit patterns, on the GPU, with the kernels' own compiler
+// division 1.0f / x over all 2^32 fp32 bit patterns, and of the XORWOW draw mappings against
+// their two-operation forms over all 2^32 draws, on the GPU, with the kernels' own compiler
 // flags.  Prints one JSON line: mismatches of the bare Newton step per biased exponent of x, and
 // the total mismatches of rcpRN (must be 0: the guard sends every exponent outside the fast range
 // to the division).  NaN results compare equal when both are NaN.
@@ -35,6 +36,28 @@ __global__ __launch_bounds__(256) void check(uint64_t base, unsigned long long* 
     if (threadIdx.x == 0 && localRn) atomicAdd(rnMis, localRn);
 }
 
+// The XORWOW draw mappings (pt_math.hpp): uniformOf(x) == (float)x * 2^-32 + 2^-33 and
+// centered2Of(u) == (u - 0.5f) * 2.0f, each against the separately rounded operations, for all
+// 2^32 draws x.
+// (scale = 2^-32 and two = 2.0f arrive as kernel arguments, so the compiler keeps the
+// two-operation forms as written.)
+__global__ __launch_bounds__(256) void checkDraws(uint64_t base, unsigned long long* mis, float scale, float two) {
+    unsigned long long mu = 0ull, mc = 0ull;
+    const uint64_t first = base + ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u;
+    for (int k = 0; k < 16; k++) {
+        const uint32_t x = (uint32_t)(first + (uint64_t)k);
+        const float prod = (float)x * scale;
+        const float u = prod + 0x1p-33f;
+        const float half = u - 0.5f;
+        const float c = half * two;
+        const float uf = uniformOf(x), cf = centered2Of(uf);
+        mu += __float_as_uint(uf) != __float_as_uint(u) ? 1ull : 0ull;
+        mc += __float_as_uint(cf) != __float_as_uint(c) ? 1ull : 0ull;
+    }
+    if (mu) atomicAdd(&mis[0], mu);
+    if (mc) atomicAdd(&mis[1], mc);
+}
+
 int main() {
     unsigned long long *dExp = nullptr, *dRn = nullptr;
     if (hipMalloc(&dExp, 256 * sizeof(unsigned long long)) != hipSuccess ||
@@ -47,6 +70,15 @@ int main() {
     const uint64_t perLaunch = 1ull << 28;   // 2^28 patterns: 65,536 blocks of 256 threads x 16
     for (uint64_t base = 0; base < (1ull << 32); base += perLaunch) {
         hipLaunchKernelGGL(check, dim3((unsigned)(perLaunch / (256 * 16))), dim3(256), 0, 0, base, dExp, dRn);
+    }
+    unsigned long long* dDraw = nullptr;
+    if (hipMalloc(&dDraw, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        fprintf(stderr, "hipMalloc failed\n");
+        return 2;
+    }
+    (void)hipMemset(dDraw, 0, 2 * sizeof(unsigned long long));
+    for (uint64_t base = 0; base < (1ull << 32); base += perLaunch) {
+        hipLaunchKernelGGL(checkDraws, dim3((unsigned)(perLaunch / (256 * 16))), dim3(256), 0, 0, base, dDraw, 0x1p-32f, 2.0f);
     }
     if (hipDeviceSynchronize() != hipSuccess) {
         fprintf(stderr, "kernel failed\n");
@@ -65,6 +97,9 @@ int main() {
         first = false;
         if ((uint32_t)e >= kRcpExpLo && (uint32_t)e <= kRcpExpHi) inRange += hExp[e];
     }
-    printf("}, \"newton_mismatches_in_fast_range\": %llu}\n", inRange);
-    return (hRn == 0 && inRange == 0) ? 0 : 1;
+    unsigned long long hDraw[2] = {0ull, 0ull};
+    (void)hipMemcpy(hDraw, dDraw, sizeof(hDraw), hipMemcpyDeviceToHost);
+    printf("}, \"newton_mismatches_in_fast_range\": %llu, \"uniform_fma_mismatches\": %llu, "
+           "\"centered2_fma_mismatches\": %llu}\n", inRange, hDraw[0], hDraw[1]);
+    return (hRn == 0 && inRange == 0 && hDraw[0] == 0 && hDraw[1] == 0) ? 0 : 1;
 }

@@ -26,6 +26,7 @@ def analyse(t: np.ndarray, slots: int) -> dict:
             "time_at_<90%_peak": float((conc < 0.9 * conc.max()).mean()),
             "time_at_<50%_peak": float((conc < 0.5 * conc.max()).mean()),
             "last_start_ms": start.max() / 1e5,
+            "end_pct_ms": {str(q): float(np.percentile(end, q) / 1e5) for q in (1, 10, 50, 90, 99, 100)},
             "xcc_span_ms": [float((end[(t[:, 2] >> 32) == x].max() - start[(t[:, 2] >> 32) == x].min()) / 1e5)
                             for x in range(8) if ((t[:, 2] >> 32) == x).any()]}
 
