@@ -219,6 +219,18 @@ struct Prim { float4 p0, p1, p2; };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rawRsrc(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1 /* 4 GB of records */, 0x00020000);
 }
+// Integer products by small constants as full-rate shifts.  v_mul_lo_u32 (and the 64-bit
+// v_mad_u64_u32) issue at a quarter of the VALU rate; LLVM folds `(x << a) + (x << b)` back into
+// a multiply and lowers it with v_mul_lo_u32, so one shift is done in an (empty-effect) asm
+// statement the folder cannot see through.
+template <int S>
+__device__ __forceinline__ uint32_t shlOpaque(uint32_t x) {
+    uint32_t t;
+    asm("v_lshlrev_b32 %0, %1, %2" : "=v"(t) : "i"(S), "v"(x));
+    return t;
+}
+__device__ __forceinline__ uint32_t mul80(uint32_t x) { return shlOpaque<6>(x) + (x << 4); }   // x < 2^26
+__device__ __forceinline__ uint32_t mul48(uint32_t x) { return shlOpaque<5>(x) + (x << 4); }   // x < 2^27
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
@@ -407,14 +419,18 @@ __device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4
     const uint32_t nearX[2] = {sx ? n2.z : n2.x, sx ? n2.w : n2.y}, farX[2] = {sx ? n2.x : n2.z, sx ? n2.y : n2.w};
     const uint32_t nearY[2] = {sy ? n3.z : n3.x, sy ? n3.w : n3.y}, farY[2] = {sy ? n3.x : n3.z, sy ? n3.y : n3.w};
     const uint32_t nearZ[2] = {sz ? n4.z : n4.x, sz ? n4.w : n4.y}, farZ[2] = {sz ? n4.x : n4.z, sz ? n4.y : n4.w};
-    const uint32_t oct4 = oct * 0x01010101u;
+    // the octant in every byte (shifts: the multiply by 0x01010101 is a quarter-rate v_mul_lo_u32)
+    const uint32_t oct2 = oct | shlOpaque<8>(oct);
+    const uint32_t oct4 = oct2 | (oct2 << 16);
     uint32_t hits = 0u;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t meta4 = h ? n1.w : n1.z;
         // per byte: internal children (0b001_11xxx) get their slot bits XOR the ray octant
         const uint32_t inner4 = (meta4 & (meta4 << 1)) & 0x10101010u;
-        const uint32_t innerMask4 = ((inner4 << 3) >> 7) * 0xffu;
+        // 0x07 in the bytes of internal children (oct4 <= 0x07070707): 8y - y, not a multiply
+        const uint32_t inner1 = inner4 >> 4;
+        const uint32_t innerMask4 = shlOpaque<3>(inner1) - inner1;
         const uint32_t bitIndex4 = (meta4 ^ (oct4 & innerMask4)) & 0x1f1f1f1fu;
         const uint32_t childBits4 = (meta4 >> 5) & 0x07070707u;
 #pragma unroll
@@ -1281,7 +1297,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     const uint32_t child = (ng >> 8) + (bit ^ (oct & 7u));
                     ng &= ~(1u << bit);
                     if (ng & 0xffu) { my[sp * kWave] = ng; sp++; }   // sp < depth <= STACK (host check)
-                    const uint32_t off = child * 80u;
+                    const uint32_t off = mul80(child);
                     const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
                     const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
                     const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
@@ -1384,8 +1400,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (h1) { k1 = tgBase + (uint32_t)__builtin_ctz(tg); tg &= tg - 1u; }
                 // Every lane loads two records (lanes without a primitive read record 0): a
                 // conditional load would cost a zero fill of 24 registers per step
-                const float4* w0 = S.wprims + 3 * (size_t)k0;
-                const float4* w1 = S.wprims + 3 * (size_t)k1;
+                // 32-bit byte offsets off the uniform base (global loads with an SGPR base): no
+                // 64-bit address arithmetic, no quarter-rate multiply
+                const float4* w0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(k0));
+                const float4* w1 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(k1));
                 const Prim q0{w0[0], w0[1], w0[2]}, q1{w1[0], w1[1], w1[2]};
                 bool redo = false;
                 if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
@@ -1729,7 +1747,7 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 sp++;
             }
             c.visits++;
-            const uint32_t off = child * 80u;
+            const uint32_t off = mul80(child);
             const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
             const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
             const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
