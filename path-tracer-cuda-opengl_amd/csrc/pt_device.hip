@@ -73,6 +73,7 @@ struct DevScene {
     const int* iparent;      // parent of each internal LBVH node (-1 for the root)
     unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
     int nprims;
+    int hasSpheres;          // 0: triangles only (the wide kernels' LEAF tests drop the sphere tie rules)
 };
 
 struct DevCamera {
@@ -372,14 +373,18 @@ __device__ __forceinline__ SlabHit refLeafBox(const Prim& q, bool sphere, float3
 // the outcome depends on the order exactly when another candidate's t lies in [t, lo).  Such a
 // lane sets `redo` and its query is repeated in the reference's order (traceRefStackless);
 // `bestLo` is the current best's window end (its box entry when t < lo, else -inf).
+// SPH = false: the scene has no spheres (DevScene::hasSpheres), so neither q nor the current best
+// is one and the tie rule reduces to the triangles' ascending rank -- the same decisions with
+// fewer instructions.
+template <bool SPH>
 __device__ __forceinline__ void wideTest(const Prim& q, float3 o, float3 d, float3 inv, float tmin, float& closest,
                                          int& best, float& bestLo, bool leafBoxes, bool& redo) {
-    const bool sph = __float_as_uint(q.p2.w) != 0u;
+    const bool sph = SPH && __float_as_uint(q.p2.w) != 0u;
     const float t = primHitAny(q, sph, o, d, tmin);
     if (t >= 0.0f) {
         const int k = (int)__float_as_uint(q.p0.w);
-        const bool none = best < 0, bSph = (best & (int)kSphereBit) != 0;
-        const int bk = best & (int)kPrimMask;
+        const bool none = best < 0, bSph = SPH && (best & (int)kSphereBit) != 0;
+        const int bk = SPH ? best & (int)kPrimMask : best;
         const bool tie = sph ? (none || !bSph || k > bk) : (!none && !bSph && k < bk);
         redo = redo || (t >= closest && t < bestLo);   // not better, but inside the current best's window
         if (t < closest || (t == closest && tie)) {
@@ -980,6 +985,7 @@ __device__ __forceinline__ DevScene ldScene(KArgs k) {
     S.nodes = k->S.nodes; S.prims = k->S.prims; S.shade = k->S.shade; S.mats = k->S.mats;
     S.wnodes = k->S.wnodes; S.wprims = k->S.wprims; S.wshade = k->S.wshade; S.rankOf = k->S.rankOf;
     S.iparent = k->S.iparent; S.err = k->S.err; S.nprims = k->S.nprims;
+    S.hasSpheres = k->S.hasSpheres;
     return S;
 }
 
@@ -1406,8 +1412,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 const float4* w1 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(k1));
                 const Prim q0{w0[0], w0[1], w0[2]}, q1{w1[0], w1[1], w1[2]};
                 bool redo = false;
-                if (h0) wideTest(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
-                if (h1) wideTest(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                if (kargs()->S.hasSpheres) {   // (uniform: read where needed)
+                    if (h0) wideTest<true>(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                    if (h1) wideTest<true>(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                } else {
+                    if (h0) wideTest<false>(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                    if (h1) wideTest<false>(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                }
                 if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
                 if (SPEC && tg == 0u && (oct & 48u)) {   // this group is done: the last parked one is next
                     oct -= 16u;
@@ -1731,7 +1742,8 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 const Prim q{w[0], w[1], w[2]};
                 if (__float_as_uint(q.p2.w) != 0u) c.spheres++;
                 else c.tris++;
-                wideTest(q, o, d, inv, tmin, closest, best, bestLo, S.nprims > 1, redo);
+                if (S.hasSpheres) wideTest<true>(q, o, d, inv, tmin, closest, best, bestLo, S.nprims > 1, redo);
+                else wideTest<false>(q, o, d, inv, tmin, closest, best, bestLo, S.nprims > 1, redo);
             }
             if ((ng & 0xffu) == 0u) {
                 if (sp == 0) break;
@@ -2179,6 +2191,7 @@ int stackFor(int depth) {
 struct pt_scene {
     int device = 0;
     int64_t nobj = 0, nmat = 0;
+    bool hasSpheres = false;                // any sphere ever in the scene (sticky across updates)
     std::vector<pt_object> objs;            // host copy (PT_BVH_HOST_KEYS path)
     DevBuf dobjs;                           // the objects on the device (BVH build input)
     DevBuf mats, nodes, prims, shade, counters;
@@ -2417,6 +2430,7 @@ DevScene devScene(const pt_scene* s) {
     S.iparent = s->iparent.as<int>();
     S.err = reinterpret_cast<unsigned int*>(s->counters.as<unsigned long long>() + 7);
     S.nprims = (int)s->nobj;
+    S.hasSpheres = s->hasSpheres ? 1 : 0;
     return S;
 }
 
@@ -2465,6 +2479,7 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
     s->nobj = n;
     s->nmat = nmat;
     s->objs.assign(objs, objs + n);
+    for (int64_t i = 0; i < n && !s->hasSpheres; i++) s->hasSpheres = objs[i].type == PT_SPHERE;
     // materials: (albedo.xyz, fuzz), (ir, type, 0, 0)
     std::vector<float4> m((size_t)std::max<int64_t>(1, 2 * nmat));
     for (int64_t i = 0; i < nmat; i++) {
@@ -2496,6 +2511,7 @@ int pt_scene_update_objects(pt_scene* s, const pt_object* objs, int64_t first, i
     if (rc) return rc;
     if (n == 0) return PT_OK;
     std::copy(objs, objs + n, s->objs.begin() + first);
+    for (int64_t i = 0; i < n && !s->hasSpheres; i++) s->hasSpheres = objs[i].type == PT_SPHERE;
     HIP_TRY(hipMemcpy(s->dobjs.as<pt_object>() + first, objs, (size_t)n * sizeof(pt_object), hipMemcpyHostToDevice));
     s->built = false;   // the hierarchy no longer matches the objects: rebuild before rendering
     s->updated = true;  // from now on the wide tree is built on the device (once per rebuild)
