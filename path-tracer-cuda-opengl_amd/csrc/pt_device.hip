@@ -1415,9 +1415,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (kargs()->S.hasSpheres) {   // (uniform: read where needed)
                     if (h0) wideTest<true>(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                     if (h1) wideTest<true>(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                    const bool s0 = __float_as_uint(q0.p2.w) != 0u, s1 = __float_as_uint(q1.p2.w) != 0u;
+                    sTris += (uint32_t)__popcll(__ballot(h0 && !s0)) + (uint32_t)__popcll(__ballot(h1 && !s1));
+                    sSph += (uint32_t)__popcll(__ballot(h0 && s0)) + (uint32_t)__popcll(__ballot(h1 && s1));
                 } else {
                     if (h0) wideTest<false>(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
                     if (h1) wideTest<false>(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                    sTris += (uint32_t)__popcll(__ballot(h0)) + (uint32_t)__popcll(__ballot(h1));
                 }
                 if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
                 if (SPEC && tg == 0u && (oct & 48u)) {   // this group is done: the last parked one is next
@@ -1426,9 +1430,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     tgBase = pend[(2u * c) * kWave + lane];
                     tg = pend[(2u * c + 1u) * kWave + lane];
                 }
-                const bool s0 = __float_as_uint(q0.p2.w) != 0u, s1 = __float_as_uint(q1.p2.w) != 0u;
-                sTris += (uint32_t)__popcll(__ballot(h0 && !s0)) + (uint32_t)__popcll(__ballot(h1 && !s1));
-                sSph += (uint32_t)__popcll(__ballot(h0 && s0)) + (uint32_t)__popcll(__ballot(h1 && s1));
             } else {
             // Every lane tests all of its queued leaves, in order, in this step (the queue then
             // is empty and the lane rejoins NODE steps; measured -4 % vs one leaf per step).
