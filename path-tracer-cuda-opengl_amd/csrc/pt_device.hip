@@ -278,8 +278,11 @@ __device__ __forceinline__ float primHitT(const Prim& q, bool sphere, float3 o, 
     float t = dot3(s2, e2) * inv;
     float b1 = dot3(s1, s) * inv;
     float b2 = dot3(s2, d) * inv;
-    if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 <= 0.0f || b1 + b2 >= 1.0f ||
-        t <= tmin || t >= closest)
+    // The reference's strict tests (cuda_object.h:83) without `b1 + b2 <= 0`, which never decides:
+    // a sum that is <= 0 is not NaN, so neither term is, and the rounded sum of two positive terms
+    // is positive -- one of b1 <= 0, b2 <= 0 already rejected it.  (b1 >= 1 and b2 >= 1 stay: with
+    // the other term NaN, the sum test would not see them.)
+    if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 >= 1.0f || t <= tmin || t >= closest)
         return -1.0f;
     return t;
 }
@@ -337,7 +340,7 @@ __device__ __forceinline__ float primHitAny(const Prim& q, bool sphere, float3 o
     float t = dot3(s2, e2) * inv;
     float b1 = dot3(s1, s) * inv;
     float b2 = dot3(s2, d) * inv;
-    if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 <= 0.0f || b1 + b2 >= 1.0f || t <= tmin)
+    if (b1 >= 1.0f || b1 <= 0.0f || b2 >= 1.0f || b2 <= 0.0f || b1 + b2 >= 1.0f || t <= tmin)   // (as primHitT)
         return -1.0f;
     return t;
 }
