@@ -98,6 +98,25 @@ def pmc_traffic(workload: str, spp: int, rng: str, kernel: str):
     return t["traffic_bytes_per_launch"], t["source"]
 
 
+# VALU issue ceiling: 256 CUs x 4 SIMDs, each issuing one wave64 VALU instruction per 2 cycles
+# (MI355X_MICROARCH.md: 32 lanes/cycle x 2) at the 2.4 GHz maximum clock
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
+
+
+def pmc_valu(workload: str, spp: int, rng: str, kernel: str):
+    """VALU wave-instructions per launch of the render kernel on this exact workload, from the
+    committed rocprofv3 pass (profiles/valu.json, tools/collect_profile.py); None if absent or for
+    another configuration."""
+    try:
+        v = json.load(open(os.path.join(REPO, "profiles", "valu.json")))
+    except (OSError, ValueError):
+        return None, None
+    if (v.get("workload") != workload or v.get("spp") != spp or v.get("rng") != rng or
+            v.get("kernel") != kernel):
+        return None, None
+    return v["valu_wave_instructions_per_launch"], v["source"]
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -257,6 +276,7 @@ def main() -> None:
                      f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
                     "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)")
         traffic, traffic_src = pmc_traffic(workload, spp, rng_desc, args.kernel)
+        valu, valu_src = pmc_valu(workload, spp, rng_desc, args.kernel)
         kernel_s = kms / 1e3 / args.steps if kms > 0 else 0.0
         hbm_gbs = traffic / kernel_s / 1e9 if (traffic and kernel_s > 0) else None
         out = {
@@ -300,7 +320,14 @@ def main() -> None:
                                                "kernel, warmup step 1): 56 B per binary node visit + 40 B per "
                                                "triangle test + 20 B per sphere test"),
                          "node_visits_reference": ref_st.node_visits,
-                         "node_visits_kernel": spec_visits / args.steps},
+                         "node_visits_kernel": spec_visits / args.steps,
+                         # the kernel's binding resource: VALU instruction
+                         # issue, its wave-instructions per launch (PMC) / kernel time vs the ceiling
+                         "valu_issue": {"achieved": (valu / kernel_s / 1e9) if (valu and kernel_s > 0) else None,
+                                        "peak": VALU_PEAK_GINST, "unit": "G wave-instructions/s",
+                                        "frac": (valu / kernel_s / 1e9 / VALU_PEAK_GINST)
+                                        if (valu and kernel_s > 0) else None,
+                                        "wave_instructions_per_launch": valu, "source": valu_src}},
         }
         if compat:
             out["compat_mode"] = compat

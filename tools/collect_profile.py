@@ -34,8 +34,9 @@ def main(tag):
         lines = f.readlines()
         g.write(lines[0])
         g.writelines(l for l in lines[1:] if "render" in l or "resolve" in l)
-    for p in ("fetch", "write", "tcc", "sq"):
-        shutil.copy(os.path.join(src, f"pmc_{p}", "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
+    for p in ("fetch", "write", "tcc", "sq", "valu"):
+        if os.path.exists(os.path.join(src, f"pmc_{p}", "run_counter_collection.csv")):
+            shutil.copy(os.path.join(src, f"pmc_{p}", "run_counter_collection.csv"), os.path.join(dst, f"pmc_{p}.csv"))
 
     bench = json.loads(open(os.path.join(src, "bench.json")).read())
     fetch = render_launches(os.path.join(dst, "pmc_fetch.csv"), "FETCH_SIZE")
@@ -56,6 +57,18 @@ def main(tag):
     with open(os.path.join(REPO, "profiles", "traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
+    # VALU wave-instructions per launch of the timed (wavefront) render kernel: the wide kernel's
+    # binding resource, reported by bench.py as roofline.valu_issue
+    valu_csv = os.path.join(dst, "pmc_valu.csv")
+    if os.path.exists(valu_csv):
+        valu = [v for k, v in render_launches(valu_csv, "SQ_INSTS_VALU") if "renderKernelWF" in k]
+        if valu:
+            v = {key: out[key] for key in ("workload", "spp", "rng", "kernel")}
+            v["valu_wave_instructions_per_launch"] = valu[-1]
+            v["source"] = f"profiles/{tag}/pmc_valu.csv (rocprofv3 --pmc SQ_INSTS_VALU, one frame)"
+            with open(os.path.join(REPO, "profiles", "valu.json"), "w") as f:
+                json.dump(v, f, indent=1)
+            print(json.dumps(v, indent=1))
 
 
 if __name__ == "__main__":

@@ -2,7 +2,7 @@
 # Bench + rocprofv3 session on the GPU box (run via gpurun).  TAG names the output dir.
 #  1. python bench.py (the driver's default command)          -> gpurun_out/$TAG/bench.json
 #  2. rocprofv3 --kernel-trace --stats of the same command      -> gpurun_out/$TAG/trace/
-#  3. separate --pmc passes (FETCH_SIZE | WRITE_SIZE | TCC hit/miss | SQ) on one frame
+#  3. separate --pmc passes (FETCH_SIZE | WRITE_SIZE | TCC hit/miss | SQ | VALU instructions) on one frame
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -25,4 +25,5 @@ step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
 step pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $OUT/pmc_tcc -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
 step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY -d $OUT/pmc_sq -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
+step pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES -d $OUT/pmc_valu -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
 echo all-ok
