@@ -1,8 +1,8 @@
 """Benchmark: Mray/s + ms/frame on bunny-in-Cornell 1920x1080 @1024spp (BASELINE.json configs[2]).
 
 One step = one full frame of the path-tracing hot path (render kernel over all pixels x spp,
-every bounce's closest-hit traversal + BSDF scatter) followed, for N > 1, by the RCCL
-all-gather of the rows to rank 0.  The frame is split into interleaved 8-row stripes across
+every bounce's closest-hit traversal + BSDF scatter) followed, for N > 1, by one RCCL gather
+of the ranks' rows to rank 0.  The frame is split into interleaved 8-row stripes across
 the N ranks (stripe s -> rank s % N), so the total work is fixed as N grows ("strong").
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5] [--spp S]
@@ -25,8 +25,12 @@ ranks) / max-over-ranks wall time of the K timed frames.  `roofline.achieved` = 
 bytes of the traversed tree (per node visit its child boxes and refs -- 56 B
 binary, 80 B 8-wide compressed -- + 40 B per triangle test + 20 B per sphere test) / render-kernel
 time from HIP events on the render stream, against the L2 ceiling (the tree is L2-resident; the
-HBM fraction of the PMC traffic is reported beside it).  `cpu_baseline` = the CPU restatement
-(oracle/) on the host cores, rank 0 at N = 1 only, on a bounded sample.
+HBM fraction of the PMC traffic is reported beside it).  PMC-derived fields (traffic, VALU
+instructions) come from the committed profiles of the SAME libpt.so build (`build_id`, sha256),
+else null.  `cpu_baseline` = the CPU restatement (oracle/) on the host cores, rank 0 at N = 1 only,
+on a bounded sample.  `interactive` (N = 1) = frames/s of the progressive interactive mode at
+1 / 4 / 16 spp.  Every timed frame is compared with the reference-order kernel's frame (pixels
+and rays).
 """
 import argparse
 import json
@@ -83,19 +87,27 @@ def cpu_baseline(preset, budget_s: float = 12.0) -> dict:
                       f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads"}
 
 
-def pmc_traffic(workload: str, spp: int, rng: str, kernel: str):
-    """Per-launch HBM traffic of the render kernel on this exact workload, from the committed
-    rocprofv3 PMC passes (profiles/traffic.json, written by tools/collect_profile.py); None if the
-    profile is for a different configuration or kernel."""
-    path = os.path.join(REPO, "profiles", "traffic.json")
+def build_id() -> str:
+    """sha256 (16 hex digits) of the libpt.so this process loaded: the committed PMC profiles carry
+    the id of the build they measured, and their counters are reported only for that build."""
+    import hashlib
+    with open(ptamd.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def pmc_entry(name: str, workload: str, spp: int, rng: str, kernel: str, build: str):
+    """The committed rocprofv3 PMC figures (profiles/<name>.json, written by tools/collect_profile.py:
+    one entry per workload) for exactly this workload, sample count, RNG mode, kernel AND library
+    build; None otherwise -- counters of another build are never paired with this build's times."""
     try:
-        t = json.load(open(path))
+        entries = json.load(open(os.path.join(REPO, "profiles", name + ".json")))
     except (OSError, ValueError):
-        return None, None
-    if (t.get("workload") != workload or t.get("spp") != spp or t.get("rng") != rng or
-            t.get("kernel", "wavefront") != kernel):
-        return None, None
-    return t["traffic_bytes_per_launch"], t["source"]
+        return None
+    for e in entries.get("entries", []):
+        if (e.get("workload") == workload and e.get("spp") == spp and e.get("rng") == rng and
+                e.get("kernel") == kernel and e.get("build_id") == build):
+            return e
+    return None
 
 
 # VALU issue ceiling: 256 CUs x 4 SIMDs, each issuing one wave64 VALU instruction per 2 cycles
@@ -103,18 +115,35 @@ def pmc_traffic(workload: str, spp: int, rng: str, kernel: str):
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
 
 
-def pmc_valu(workload: str, spp: int, rng: str, kernel: str):
-    """VALU wave-instructions per launch of the render kernel on this exact workload, from the
-    committed rocprofv3 pass (profiles/valu.json, tools/collect_profile.py); None if absent or for
-    another configuration."""
-    try:
-        v = json.load(open(os.path.join(REPO, "profiles", "valu.json")))
-    except (OSError, ValueError):
-        return None, None
-    if (v.get("workload") != workload or v.get("spp") != spp or v.get("rng") != rng or
-            v.get("kernel") != kernel):
-        return None, None
-    return v["valu_wave_instructions_per_launch"], v["source"]
+def interactive(scene, preset, dev, stream, local, frames=(30, 20, 10), spps=(1, 4, 16)) -> dict:
+    """The reference's second product mode (renderToGL, main.cu:489-528: camera movement via
+    camera::processKeyboard, camera.h:41-56, then a frame rendered into an RGBA8 surface),
+    made progressive: per display frame one camera move, the accumulation restarted
+    (pt_film_clear), `spp` samples accumulated and converted to RGBA8 on the device
+    (PT_OUT_RGBA8_SURFACE).  Frames are enqueued without host synchronisation (pt_render_ex
+    without pt_stats); frames/s = frames / wall time from the first enqueue to the last frame
+    done."""
+    w, h = preset.width, preset.height
+    film = ptamd.Film(w, h, 1, device=local)
+    buf = torch.empty((w * h * 4,), dtype=torch.uint8, device=dev)
+    cam = ptamd.Camera.from_buffer_copy(bytes(preset.camera))
+    out = {}
+    for spp, n in zip(spps, frames):
+        for it in range(2):   # warm (tile order, allocations), then timed
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for k in range(n):
+                ptamd.camera_move(cam, (0, 2, 1, 3)[k % 4], 0.01)   # forward, left, back, right
+                film.clear(stream.cuda_stream)
+                ptamd.render(scene, film, cam, spp, preset.max_depth, out=buf.data_ptr(), stream=stream.cuda_stream,
+                             rng=ptamd.RNG_SAMPLE, accumulate=True, out_format=ptamd.OUT_RGBA8_SURFACE, wait=False)
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+        st = film.stats()
+        out[f"{spp}spp"] = {"fps": n / el, "ms_per_frame": el / n * 1e3, "frames": n,
+                            "rays_per_frame": st.rays, "kernel_ms": st.kernel_ms}
+    film.close()
+    return out
 
 
 def main() -> None:
@@ -134,6 +163,8 @@ def main() -> None:
                          "reference's per-pixel cuRAND-XORWOW streams (a pixel's 1024 samples are sequential)")
     ap.add_argument("--chunk", type=int, default=0, help="sample mode: summation block (0 = library default)")
     ap.add_argument("--no-compat", action="store_true", help="skip the compat-mode reference frame (N = 1)")
+    ap.add_argument("--no-interactive", action="store_true",
+                    help="skip the interactive-mode frames/s at 1 / 4 / 16 spp (N = 1)")
     ap.add_argument("--output", default="rgba8", choices=["rgba8", "f32"],
                     help="frame format rendered and gathered: rgba8 (default: quantised on the device like "
                          "PngImage::saveColor, 4 B/pixel on the wire) or f32 (linear-sqrt RGB, 12 B/pixel)")
@@ -174,7 +205,8 @@ def main() -> None:
     chans, tdt = (4, torch.uint8) if rgba8 else (3, torch.float32)
     out_format = ptamd.OUT_RGBA8 if rgba8 else ptamd.OUT_RGB32F
     local_buf = torch.zeros((max_rows * w * chans,), dtype=tdt, device=dev)
-    gathered = torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if world > 1 else None
+    ref_buf = torch.zeros_like(local_buf)   # the reference-order kernel's frame (warmup step 1)
+    gathered = torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if world > 1 and rank == 0 else None
     stream = torch.cuda.current_stream(dev)
 
     sample = args.rng == "sample"
@@ -190,13 +222,13 @@ def main() -> None:
                              stream=stream.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
                              shade_batch=args.shade_batch, rng=ptamd.RNG_SAMPLE if sample else ptamd.RNG_COMPAT,
                              chunk=args.chunk, out_format=out_format)
-        if world > 1:
+        if world > 1:   # the frame's stripes to rank 0 (one gather; SURVEY 8(e) ncclGather)
             if backend == "nccl":
-                dist.all_gather_into_tensor(gathered, local_buf)
+                ptdist.gather_to_root(local_buf, world, rank, gathered)
             else:
-                parts = [torch.empty_like(local_buf, device="cpu") for _ in range(world)]
-                dist.all_gather(parts, local_buf.cpu())
-                gathered.copy_(torch.cat(parts))
+                g = ptdist.gather_to_root(local_buf.cpu(), world, rank)
+                if rank == 0:
+                    gathered.copy_(g)
         return st
 
     # Warmup 1 uses the ray-synchronous kernel, whose traversal follows the reference's node
@@ -204,6 +236,7 @@ def main() -> None:
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
     ref_st = frame(ptamd.KERNEL_SIMPLE)
+    ref_buf.copy_(local_buf)
     for _ in range(max(0, args.warmup - 1)):
         frame()
     if args.kernel == "wide":   # the wide tree was built at the first wide render (host binned SAH)
@@ -217,8 +250,10 @@ def main() -> None:
     spec_visits = 0
     for _ in range(args.steps):
         st = frame()
-        if st.rays != ref_st.rays or (args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
-                                                                      st.sphere_tests != ref_st.sphere_tests)):
+        # every timed frame: this rank's pixels and ray count equal the reference-order frame's
+        if st.rays != ref_st.rays or not torch.equal(local_buf, ref_buf) or (
+                args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
+                                                st.sphere_tests != ref_st.sphere_tests)):
             raise SystemExit("frame differs from the reference-order frame")
         rays += st.rays
         # algorithmic bytes of the tree the kernel traverses: the wide kernel's own visits; the
@@ -275,8 +310,11 @@ def main() -> None:
         rng_desc = (("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
                      f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
                     "cuRAND-XORWOW semantics, curand_init(seed, pixel, 0)")
-        traffic, traffic_src = pmc_traffic(workload, spp, rng_desc, args.kernel)
-        valu, valu_src = pmc_valu(workload, spp, rng_desc, args.kernel)
+        bid = build_id()
+        te = pmc_entry("traffic", workload, spp, rng_desc, args.kernel, bid)
+        ve = pmc_entry("valu", workload, spp, rng_desc, args.kernel, bid)
+        traffic, traffic_src = (te["traffic_bytes_per_launch"], te["source"]) if te else (None, None)
+        valu, valu_src = (ve["valu_wave_instructions_per_launch"], ve["source"]) if ve else (None, None)
         kernel_s = kms / 1e3 / args.steps if kms > 0 else 0.0
         hbm_gbs = traffic / kernel_s / 1e9 if (traffic and kernel_s > 0) else None
         out = {
@@ -304,7 +342,10 @@ def main() -> None:
             # L2-resident: its bytes come from L2 and L1, HBM traffic is the per-task block sums
             # (`hbm`, PMC).  The applicable memory ceiling is L2 bandwidth; the measured ceiling of
             # this access pattern (dependent per-lane gathers) is `gather_ceiling`.
-            "roofline": {"bound": "l2", "achieved": achieved, "peak": L2_PEAK_GBS, "unit": "GB/s",
+            # (the memory level whose ceiling `achieved` is held against; the resource that binds
+            # the kernel is VALU issue with partly idle lanes -- `limiter`, `valu_issue`)
+            "roofline": {"bound": "l2", "limiter": "valu_issue", "achieved": achieved, "peak": L2_PEAK_GBS,
+                         "unit": "GB/s",
                          "frac": achieved / L2_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
@@ -329,8 +370,11 @@ def main() -> None:
                                         if (valu and kernel_s > 0) else None,
                                         "wave_instructions_per_launch": valu, "source": valu_src}},
         }
+        out["build_id"] = bid
         if compat:
             out["compat_mode"] = compat
+        if world == 1 and not args.no_interactive:
+            out["interactive"] = interactive(scene, preset, dev, stream, local)
         if world == 1:   # the per-frame rebuild of a dynamic scene: LBVH + wide tree, both on the device
             dyn = ptamd.Scene(preset.objects, preset.materials, device=local,
                               flags=ptamd.PT_BVH_ORIGIN_BOUNDS | ptamd.PT_BVH_WIDE_DEVICE)

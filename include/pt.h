@@ -135,6 +135,10 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n_objects,
  * same images. */
 #define PT_BVH_WIDE_DEVICE 4
 int pt_scene_build_bvh(pt_scene* scene, int flags);
+/* pt_scene_build_bvh with its device work enqueued on `stream` (a hipStream_t, NULL = the null
+ * stream) instead of the null stream; returns when the build is complete (the tree depth is read
+ * back to pick the traversal kernel). */
+int pt_scene_build_bvh_ex(pt_scene* scene, int flags, void* stream);
 /* Dynamic scenes (per-frame rebuild): overwrite objects [first, first + n)
  * (host array; same validation as pt_scene_create) and mark the hierarchy stale -- rendering or
  * tracing fails with PT_ERR_STATE until pt_scene_build_bvh runs again.  A rebuild reuses every
@@ -175,7 +179,12 @@ int pt_film_set_rng(pt_film* film, const uint32_t* states);
 /* render<<<>>> (main.cu:271-294): spp samples per pixel of the film's rows, max_depth bounces.
  * Writes sqrt(mean) RGB, 3 floats per pixel, local rows in order.  out_rgb is a device
  * pointer when out_on_device != 0 (then `stream` is the hipStream_t to use, may be NULL),
- * else a host pointer.  The film's RNG streams advance, as the reference's devStates do. */
+ * else a host pointer.  The film's RNG streams advance, as the reference's devStates do.
+ * Asynchronous when out_on_device != 0 and stats == NULL: the call enqueues the frame's kernels
+ * (render, resolve, the next launch's tile order) on `stream` and returns without waiting for the
+ * device; pt_film_stats() then gives the frame's counters.  With stats != NULL, or a host output,
+ * the call returns when the frame is done.  Frames of one film must use one stream (or be ordered
+ * by the caller): the film's buffers are reused by the next frame. */
 int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
               float* out_rgb, int out_on_device, void* stream, pt_stats* stats);
 /* Render options.
@@ -192,11 +201,13 @@ int pt_render(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int
  *   PT_RNG_SAMPLE: one XORWOW stream per pixel-sample (the reference's generator and
  *   curand_uniform mapping), its state seeded by one Philox4x32-10 block with key = film seed and
  *   counter = {sample, pixel, 0, "SAMP"}; samples are summed in blocks of `chunk` samples
- *   (0 = max(16, ceil(spp/64))) and the block sums are added in order.  (pixel, block) tasks
- *   are handed to persistent waves, longest tiles first from the previous launch's costs; the
- *   scheduling never changes the image.  Deterministic, statistically identical to the
- *   reference, not its random numbers; does not advance the film's XORWOW streams.  Needs
- *   chunk-count x pixels x 16 bytes of device memory for the block partials {sum xyz, rays}.
+ *   (0 = max(16, ceil(spp/64))), each block's fp32 sum is converted to 32.32 fixed point and the
+ *   pixel's blocks are added exactly (integer atomics: the order in which blocks finish does not
+ *   matter).  (pixel, block) tasks are handed to persistent waves, longest tiles first from the
+ *   previous launch's costs; neither the scheduling nor the stripe partition changes the image.
+ *   Deterministic, statistically identical to the reference, not its random numbers; does not
+ *   advance the film's XORWOW streams.  Needs 32 bytes of device memory per pixel
+ *   ({x, y, z, rays} accumulators), whatever the spp.
  *   The wide kernel builds its tree on the host at the first render after each
  *   pt_scene_build_bvh (C3 5,000 triangles ~5 ms, C5 1.04 M ~0.8 s) unless the build was asked
  *   for PT_BVH_WIDE_DEVICE (the tree built on the device, milliseconds), or on the device at
@@ -227,6 +238,9 @@ typedef struct {
 int pt_render_ex(pt_scene* scene, pt_film* film, const pt_camera* cam, int spp, int max_depth,
                  float* out_rgb, int out_on_device, void* stream, const pt_render_opts* opts,
                  pt_stats* stats);
+/* Work counters and kernel time of the film's last pt_render / pt_render_ex; waits for that
+ * frame to finish.  Reports PT_ERR_STATE if a traversal guard tripped in it (corrupt tree). */
+int pt_film_stats(pt_film* film, pt_stats* stats);
 /* Re-initialise the film's streams to their initRandom state (asynchronous on `stream`). */
 int pt_film_reset(pt_film* film, void* stream);
 /* Progressive rendering: zero the film's accumulated sums (asynchronous on `stream`); the number

@@ -297,6 +297,16 @@ inline void sampleStream(uint64_t seed, uint32_t sample, uint64_t pixel, uint32_
     st[4] = w[3] ^ 0x6C078965u;
     st[5] = w[0] ^ w[1] ^ 0x2545F491u;
 }
+// Sample mode: a chunk's fp32 sum as a 32.32 fixed-point integer (truncated toward zero; NaN -> 0,
+// saturated at +-2^62).  Integer sums do not depend on the order of addition, so the device can
+// add a pixel's chunks with atomics in whatever order its tasks finish.
+inline int64_t blockFixed(float x) {
+    float p = x * 4294967296.0f;   // exact: a power-of-two scale
+    if (p != p) p = 0.0f;
+    p = std::fmin(std::fmax(p, -4611686018427387904.0f), 4611686018427387904.0f);
+    return (int64_t)p;
+}
+inline float fixedToFloat(int64_t a) { return (float)((double)a * 0x1p-32); }
 struct TapeRng {
     const float* tape; int len; int pos;
     float operator()() { return pos < len ? tape[pos++] : (pos++, 0.5f); }
@@ -775,8 +785,8 @@ int orc_render_sample2(const orc_object* objs, int64_t nobj, const orc_material*
             const int row = rows[ri];
             for (int col = 0; col < width; col++) {
                 const uint64_t pixel = (uint64_t)row * (uint64_t)width + (uint64_t)col;
-                V3 total{0, 0, 0};
-                for (int c0 = 0; c0 < spp; c0 += chunk) {   // chunks summed in order
+                int64_t acc[3] = {0, 0, 0};
+                for (int c0 = 0; c0 < spp; c0 += chunk) {   // each chunk summed in sample order (fp32)
                     V3 part{0, 0, 0};
                     for (int s = c0; s < std::min(spp, c0 + chunk); s++) {
                         uint32_t st[6];
@@ -784,8 +794,12 @@ int orc_render_sample2(const orc_object* objs, int64_t nobj, const orc_material*
                         XorwowRng rng{st};
                         part = part + tracePath(objs, nobj, mats, nodes, cam, col, row, invW, invH, max_depth, rng, local);
                     }
-                    total = total + part;
+                    // chunk sums added exactly (order-free): 32.32 fixed point, as the device's atomics
+                    acc[0] += blockFixed(part.x);
+                    acc[1] += blockFixed(part.y);
+                    acc[2] += blockFixed(part.z);
                 }
+                const V3 total{fixedToFloat(acc[0]), fixedToFloat(acc[1]), fixedToFloat(acc[2])};
                 const int64_t k = (int64_t)ri * width + col;
                 if (out_sum) { out_sum[3 * k + 0] = total.x; out_sum[3 * k + 1] = total.y; out_sum[3 * k + 2] = total.z; }
                 out_rgb[3 * k + 0] = std::sqrt(total.x * invSpp);

@@ -74,6 +74,7 @@ struct DevScene {
     unsigned int* err;       // set (never cleared in-kernel) when a traversal guard trips
     int nprims;
     int hasSpheres;          // 0: triangles only (the wide kernels' LEAF tests drop the sphere tie rules)
+    float cx, cy, cz, ext;   // tight scene box: centre and largest extent (the wide kernels' far-origin test)
 };
 
 struct DevCamera {
@@ -414,6 +415,11 @@ __device__ __forceinline__ void wideTest(const Prim& q, float3 o, float3 d, floa
 // inv; the planes lie a quantum outside the exact boxes, far beyond this arithmetic's rounding,
 // and a NaN (0 * inf on an axis the ray is parallel to) only drops that plane: the test never
 // rejects a box the exact slab test (aabb.h:21-34) accepts.
+//
+// The margin holds while |p - o| stays within about 11 times the larger of the scene's extent
+// and its coordinates (the quantum is >= 2^-18 of that, the rounding of the ray's plane distances
+// about 2^-21.6 of |p - o|): a ray whose origin lies farther than 8 scene extents from the
+// scene's centre (wideFar) skips this test and is traced in the reference's order instead.
 __device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4 n3, uint4 n4, float3 o, float3 inv,
                                              uint32_t oct, float tmin, float tmax) {
     const float ax = __uint_as_float((n0.w & 0xffu) << 23) * inv.x;
@@ -457,6 +463,14 @@ __device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4
     }
     return hits;
 }
+
+// The ray origin lies farther than 8 scene extents from the scene's centre on some axis, beyond
+// the distance the wide boxes' margin covers (wideHits): the query runs in the reference's order.
+__device__ __forceinline__ bool wideFar(float cx, float cy, float cz, float ext, float3 o) {
+    const float m = fmaxf(fmaxf(fabsf(o.x - cx), fabsf(o.y - cy)), fabsf(o.z - cz));
+    return !(m <= 8.0f * ext);   // (NaN: far)
+}
+__device__ __forceinline__ bool wideFar(const DevScene& S, float3 o) { return wideFar(S.cx, S.cy, S.cz, S.ext, o); }
 
 // RenderManager::hitBvh (render_manager.h:86-135): same visiting order (left child, right
 // child, leaf children tested at once, internal children pushed left then right).
@@ -514,7 +528,8 @@ __device__ __forceinline__ int traceRefStackless(const DevScene& S, float3 o, fl
     }
     const float3 inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
     int node = 0, from = -1;   // from >= 0: returning from that child of `node`
-    for (int guard = 0; guard <= 2 * S.nprims; guard++) {
+    bool finished = false;
+    for (int guard = 0; guard <= 4 * S.nprims; guard++) {   // each node is entered and left once
         const float4* np = S.nodes + 4 * (size_t)node;
         const float4 a = np[0], b = np[1], q = np[2], r = np[3];
         const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
@@ -539,11 +554,12 @@ __device__ __forceinline__ int traceRefStackless(const DevScene& S, float3 o, fl
             node = next;
             from = -1;
         } else {
-            if (node == 0) break;
+            if (node == 0) { finished = true; break; }
             from = node;
             node = S.iparent[node];
         }
     }
+    if (!finished) atomicOr(S.err, 4u);   // a corrupt tree or parent links: reported, never silent
     return best;
 }
 
@@ -737,12 +753,13 @@ struct RenderParams {
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
     int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
-    // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples; the sum
-    // of block b lands in partial[b][pixel] (3 floats) and blocks are reduced in order.  Each
-    // (pixel, block) is one task, summed in sample order by whichever lane takes it, so the
-    // image does not depend on scheduling.
+    // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples.  Each
+    // (pixel, block) is one task, summed in sample order (fp32) by whichever lane takes it; the
+    // block sum is then added to the pixel's accumulator as a 32.32 fixed-point integer
+    // (blockFixed), with atomics: integer addition is exact and order-free, so the image does
+    // not depend on scheduling or on the stripe partition.  pixAcc[4 * pixel] = {x, y, z, rays}.
     int nblocks, block;
-    float* partial;
+    unsigned long long* pixAcc;
     unsigned* taskCounter;                    // next task (zeroed before the launch)
     uint32_t* stackSpill;                     // sample mode, STACK > 32: stack entries >= 32 (per wave slot, lane)
     uint32_t ntasks;                          // tile slots x nblocks x 64
@@ -752,6 +769,28 @@ struct RenderParams {
     int rawOut;                               // compat: store the raw sample sum (resolveKernel follows)
     int stripeShift, blockShift;              // log2(stripe_h), log2(block) when powers of two, else -1
 };
+
+// Sample mode: a block's fp32 sum as a 32.32 fixed-point integer (truncated toward zero; NaN -> 0,
+// saturated at +-2^62), and back (oracle/pt_oracle.cpp blockFixed / fixedToFloat, same roundings).
+// (Truncation done as two 32-bit halves of |p|: a * 2^-32 and a - hi * 2^32 are exact, hi has at
+// most 24 significant bits; fewer registers than the generic float -> int64 conversion.)
+__device__ __forceinline__ unsigned long long blockFixed(float x) {
+    const float p = x * 4294967296.0f;   // exact: a power-of-two scale
+    const float a = p == p ? fminf(fabsf(p), 0x1p62f) : 0.0f;
+    const uint32_t hi = (uint32_t)(a * 0x1p-32f);
+    const uint32_t lo = (uint32_t)__builtin_fmaf((float)hi, -0x1p32f, a);
+    const unsigned long long u = ((unsigned long long)hi << 32) | lo;
+    return p < 0.0f ? 0ull - u : u;
+}
+__device__ __forceinline__ float fixedToFloat(unsigned long long a) { return (float)((double)(long long)a * 0x1p-32); }
+// One finished (pixel, block) task: its sum and its ray count (the tile-cost input of the next
+// launch's longest-first order) added to the pixel's accumulator, no-return atomics.
+__device__ __forceinline__ void addBlock(unsigned long long* acc, float3 sum, uint32_t rays) {
+    __hip_atomic_fetch_add(acc + 0, blockFixed(sum.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(acc + 1, blockFixed(sum.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(acc + 2, blockFixed(sum.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(acc + 3, (unsigned long long)rays, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Compat mode end of a pixel: sqrt(sum / spp) (main.cu:290-293), or the raw sum when a resolve
 // pass (accumulation / 8-bit output) follows.
@@ -834,9 +873,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
         auto flush = [&]() {
             if constexpr (SAMPLE) {
                 if (sample % P.block == 0 || sample == P.spp) {
-                    float4* pp = reinterpret_cast<float4*>(P.partial) +
-                                 ((size_t)((sample - 1) / P.block) * ((size_t)P.width * P.nrows) + idx);
-                    *pp = make_float4(sum.x, sum.y, sum.z, __uint_as_float(c.rays - blockRays0 + 1u));
+                    addBlock(P.pixAcc + 4 * idx, sum, c.rays - blockRays0 + 1u);
                     blockRays0 = c.rays;
                     sum = f3(0.0f, 0.0f, 0.0f);
                 }
@@ -989,6 +1026,7 @@ __device__ __forceinline__ DevScene ldScene(KArgs k) {
     S.wnodes = k->S.wnodes; S.wprims = k->S.wprims; S.wshade = k->S.wshade; S.rankOf = k->S.rankOf;
     S.iparent = k->S.iparent; S.err = k->S.err; S.nprims = k->S.nprims;
     S.hasSpheres = k->S.hasSpheres;
+    S.cx = k->S.cx; S.cy = k->S.cy; S.cz = k->S.cz; S.ext = k->S.ext;
     return S;
 }
 
@@ -1009,6 +1047,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     constexpr int SPECN = WIDE ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
     __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
+    // sample mode: each lane's last finished block {sum, rays} and its pixel, until flushed
+    __shared__ float4 flushSum[SAMPLE ? kWave : 1];
+    __shared__ uint32_t flushPix[SAMPLE ? kWave : 1];
+    bool flushLane = false;
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1089,6 +1131,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             tg = 0u;                                                                              \
             bestLo = -__builtin_inff();                                                           \
             ng = S.nprims > 0 ? (1u << oct) : 0u;                                                 \
+            if (wideFar(kargs()->S.cx, kargs()->S.cy, kargs()->S.cz, kargs()->S.ext, o)) {         \
+                ng = 0u;       /* origin far from the scene: no wide traversal, */                 \
+                oct |= 8u;     /* the query in the reference's order (SHADE's redo) */             \
+            }                                                                                     \
         } else if (S.nprims <= 1) {                                                               \
             node = -1;                                                                            \
             if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
@@ -1164,16 +1210,28 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Sample mode: the lane's block is complete -> its sum, cost; ask for the next task.
 #define PT_FINISH_TASK()                                                                            \
     do {                                                                                          \
-        const auto& Q_ = *kargs();                                                                \
-        const uint32_t blk_ = Q_.blockShift >= 0 ? (uint32_t)(nSamples - 1) >> Q_.blockShift            \
-                                                 : (uint32_t)(nSamples - 1) / (uint32_t)Q_.block;         \
         const uint32_t c_ = cr & 0xffffu, r_ = cr >> 16;                                          \
-        float4* pp_ = reinterpret_cast<float4*>(Q_.partial) +                                      \
-                      ((size_t)blk_ * ((size_t)Q_.width * (size_t)Q_.nrows) + (size_t)(r_ * (uint32_t)Q_.width + c_)); \
-        /* one 16-B store: the block sum and the task's ray count (the tile cost, summed by the \
-           resolve pass; a per-task global atomic here cost 14 % of the frame) */              \
-        *pp_ = make_float4(sum.x, sum.y, sum.z, __uint_as_float(taskRays + 1u));                  \
+        /* the block sum and the task's ray count wait in LDS; the next loop iteration adds them \
+           to the pixel's accumulator (PT_FLUSH_BLOCKS, where few registers are live) */          \
+        flushSum[lane] = make_float4(sum.x, sum.y, sum.z, __uint_as_float(taskRays + 1u));      \
+        flushPix[lane] = r_ * (uint32_t)kargs()->width + c_;                                      \
+        flushLane = true;                                                                         \
         needTask = true;                                                                          \
+    } while (0)
+    // Finished blocks -> their pixels' accumulators: order-free integer atomics on per-pixel
+    // addresses (no contention).  At the top of the step loop, a uniform branch.
+#define PT_FLUSH_BLOCKS()                                                                           \
+    do {                                                                                          \
+        if constexpr (SAMPLE) {                                                                   \
+            if (__ballot(flushLane) != 0) {                                                       \
+                if (flushLane) {                                                                  \
+                    const float4 v_ = flushSum[lane];                                             \
+                    addBlock(kargs()->pixAcc + 4 * (size_t)flushPix[lane], f3(v_.x, v_.y, v_.z),  \
+                             __float_as_uint(v_.w));                                              \
+                }                                                                                 \
+                flushLane = false;                                                                \
+            }                                                                                     \
+        }                                                                                         \
     } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
@@ -1210,6 +1268,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     }
                     PT_FINISH_TASK();
                 }
+                PT_FLUSH_BLOCKS();
             }
             needTask = false;
         }
@@ -1261,6 +1320,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     PT_PARK();
 
     for (;;) {
+        PT_FLUSH_BLOCKS();
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
@@ -1561,6 +1621,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }
 #endif
     }
+    PT_FLUSH_BLOCKS();   // (the loop ends only when no lane has work: a block closed in its last step)
     PT_UNPARK();
     if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
         if constexpr (PARK) idx = (cr >> 16) * (uint32_t)P.width + (cr & 0xffffu);
@@ -1611,6 +1672,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK
+#undef PT_FLUSH_BLOCKS
 #undef PT_DIAG_ADD
 
 // Frame epilogue (one lane per pixel).  The frame's linear sum S is the raw compat sum
@@ -1621,27 +1683,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 // PngImage::saveColor (png_image.h:24-30: (uint8)(clamp(c, 0, 0.999) * 256), alpha 255) or like
 // renderBySurface (main.cu:327-331: (unsigned)(c * 255) into an 8-bit field, alpha 255).
 // Rows stay in film order (row 0 = bottom); the PNG writer flips them.
-// Sample mode: the partials are 16-B records {block sum xyz, rays}; the pixel's rays over all
-// blocks are added to its tile's cost (the next launch's longest-first order).
-__global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ src, int nblocks, float* accum,
+// Sample mode: the pixel's 32-B accumulator {x, y, z (32.32 fixed point), rays}; its rays are
+// added to its tile's cost (the next launch's longest-first order).
+__global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ src,
+                                                     const unsigned long long* __restrict__ pixAcc, float* accum,
                                                      float inv, int format, void* out, int64_t npix,
                                                      unsigned* tileCost, int width, int tilesX, int costMax) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix) return;
     float x, y, z;
-    if (nblocks == 0) {
+    if (!pixAcc) {
         x = src[3 * i + 0]; y = src[3 * i + 1]; z = src[3 * i + 2];
     } else {
-        x = 0.0f; y = 0.0f; z = 0.0f;
-        uint32_t rays = 0;
-        const float4* q4 = reinterpret_cast<const float4*>(src);
-        for (int c = 0; c < nblocks; c++) {
-            const float4 q = q4[(size_t)c * (size_t)npix + (size_t)i];
-            x = x + q.x;
-            y = y + q.y;
-            z = z + q.z;
-            rays += __float_as_uint(q.w);
-        }
+        const ulonglong2* a2 = reinterpret_cast<const ulonglong2*>(pixAcc + 4 * i);
+        const ulonglong2 a = a2[0], b = a2[1];
+        x = fixedToFloat(a.x);
+        y = fixedToFloat(a.y);
+        z = fixedToFloat(b.x);
+        const uint32_t rays = (uint32_t)min(b.y, 0xffffffffull);
         if (tileCost) {
             const int row = (int)(i / width), col = (int)(i - (int64_t)row * width);
             unsigned* tc = tileCost + (row >> 3) * tilesX + (col >> 3);
@@ -1674,6 +1733,16 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
         px |= b << (8 * k);
     }
     static_cast<uint32_t*>(out)[i] = px;
+}
+
+// Longest-first launch order on the device: keys ~cost (ascending = cost descending) and tile ids,
+// then a stable radix sort (pt_sort.hip): equal costs keep ascending tile ids.
+__global__ __launch_bounds__(256) void tileKeyKernel(const unsigned* __restrict__ cost, uint32_t* keys, uint32_t* ids,
+                                                     int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = ~cost[i];
+    ids[i] = (uint32_t)i;
 }
 
 // pt_trace_closest on the binary LBVH, in the reference order (trace<STACK>).
@@ -1732,11 +1801,12 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
         const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
         const float3 inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
         const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+        const bool far = wideFar(S, o);   // (then: the query in the reference's order only)
         float closest = tmax;
         int best = -1, sp = 0;
-        bool redo = false;
+        bool redo = far;
         float bestLo = -__builtin_inff();
-        uint32_t ng = S.nprims > 0 ? (1u << oct) : 0u, tgBase = 0u, tg = 0u;
+        uint32_t ng = S.nprims > 0 && !far ? (1u << oct) : 0u, tgBase = 0u, tg = 0u;
         c.rays++;
         for (;;) {
             while (tg) {
@@ -2178,6 +2248,20 @@ int envInt(const char* name, int dflt) {
     return x > 64 ? 64 : x;
 }
 
+// Events of a synchronous device step; on an early return (ok still false) the stream's queued
+// work is waited for before the caller can free or reuse what it reads.
+struct StreamGuard {
+    hipStream_t st;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool ok = false;
+    explicit StreamGuard(hipStream_t s) : st(s) {}
+    ~StreamGuard() {
+        if (!ok) (void)hipStreamSynchronize(st);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    }
+};
+
 int stackFor(int depth) {
     const int need = depth + 1;
 #if PT_STACK24
@@ -2217,6 +2301,7 @@ struct pt_scene {
     bool built = false;
     size_t deviceBytes = 0;
     double buildMs = 0.0;                   // last pt_scene_build_bvh, device time (HIP events)
+    float sceneCE[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // tight scene box: centre, largest extent (DevScene)
 };
 
 struct pt_film {
@@ -2228,16 +2313,29 @@ struct pt_film {
     DevBuf state;   // 6 x npix uint32 (SoA)
     DevBuf jumps;   // XORWOW jump matrices (for pt_film_reset)
     DevBuf tileCost, tileOrder;   // measured per-tile cost of the last launch; LPT launch order
+    DevBuf tileKeys, tileKeys2, tileIds, sortTemp;   // the order's radix sort on the device
     bool haveOrder = false;
-    std::vector<unsigned> cost;   // host copy of tileCost and the spp it was measured at
-    int costSpp = 0;
-    DevBuf partial, taskCounter;  // sample mode: per-block partial sums; task counter
+    DevBuf pixAcc, taskCounter;   // sample mode: per-pixel {x, y, z, rays} accumulators; task counter
     DevBuf stackSpill;            // sample mode on deep trees: traversal stack entries beyond LDS
-    size_t partialBytes = 0;
     DevBuf sums;                  // compat mode: raw per-pixel sample sums of the frame (resolve input)
     DevBuf accum;                 // progressive rendering: fp32 RGB running sums of every accumulated frame
+    DevBuf staging;               // device copy of a host output frame
     int64_t accumSamples = 0;     // samples per pixel in `accum`
     int cus = 0;                  // compute units of the device (persistent grid size)
+    // The last render's work counters (rays, visits, tests, paths, error word), filled by its
+    // kernels, and the events around its kernels: read by pt_film_stats (or by pt_render_ex when
+    // it is given a pt_stats), so a render with stats == NULL never waits for the device.
+    DevBuf counters;
+    unsigned long long* hostCounters = nullptr;   // pinned: the counters copied back in stream order
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;   // kernels start / end, counters copied
+    bool rendered = false;
+    bool lastWide = false;
+    ~pt_film() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (ev2) (void)hipEventDestroy(ev2);
+        if (hostCounters) (void)hipHostFree(hostCounters);
+    }
 };
 
 namespace {
@@ -2313,16 +2411,16 @@ int setDevice(int dev) {
 
 template <int S>
 void launchRenderWide(const RenderParams& P, hipStream_t st) {
-    if (P.partial) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
+    if (P.pixAcc) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
     else renderKernelWF<S, false, true><<<P.ntiles, kWave, 0, st>>>(P);
 }
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
-    if (P.kernel == PT_KERNEL_WAVEFRONT && P.partial)
+    if (P.kernel == PT_KERNEL_WAVEFRONT && P.pixAcc)
         renderKernelWF<S, true, false><<<P.nwaves, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT)
         renderKernelWF<S, false, false><<<P.ntiles, kWave, 0, st>>>(P);
-    else if (P.partial) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
+    else if (P.pixAcc) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
 template <int S, bool WIDE>
@@ -2435,6 +2533,7 @@ DevScene devScene(const pt_scene* s) {
     S.err = reinterpret_cast<unsigned int*>(s->counters.as<unsigned long long>() + 7);
     S.nprims = (int)s->nobj;
     S.hasSpheres = s->hasSpheres ? 1 : 0;
+    S.cx = s->sceneCE[0]; S.cy = s->sceneCE[1]; S.cz = s->sceneCE[2]; S.ext = s->sceneCE[3];
     return S;
 }
 
@@ -2452,6 +2551,41 @@ void fillStats(pt_stats* st, const unsigned long long c[5], double ms, bool wide
     st->paths = c[4];
     st->kernel_ms = ms;
     st->algo_bytes = (wide ? 80ull : 56ull) * c[1] + 40ull * c[2] + 20ull * c[3];
+}
+
+// Diagnostics of the wavefront scheduler (PT_ITER_STATS=1; the per-step counters need a PT_DIAG build).
+void printIterStats(const unsigned long long* c, bool wide) {
+    if (c[8] + c[9] + c[10] > 0)
+        std::fprintf(stderr, "[pt] iterations node %llu leaf %llu shade %llu | lanes/iter node %.1f leaf %.1f "
+                     "shade %.1f\n", c[8], c[9], c[10], (double)c[1] / std::max(1ull, c[8]),
+                     (double)c[11] / std::max(1ull, c[9]), (double)c[0] / std::max(1ull, c[10]));
+    if (c[12] + c[13] + c[14] > 0)
+        std::fprintf(stderr, "[pt] cycles/iteration node %.0f leaf %.0f shade %.0f | share node %.3f leaf %.3f "
+                     "shade %.3f\n", (double)c[12] / std::max(1ull, c[8]), (double)c[13] / std::max(1ull, c[9]),
+                     (double)c[14] / std::max(1ull, c[10]), (double)c[12] / (double)(c[12] + c[13] + c[14]),
+                     (double)c[13] / (double)(c[12] + c[13] + c[14]), (double)c[14] / (double)(c[12] + c[13] + c[14]));
+    if (wide && c[8] > 0)
+        std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps); NODE steps: "
+                     "lanes waiting on primitives with nodes left %.1f, lanes without NODE work %.1f\n", c[20],
+                     (double)c[21] / std::max(1ull, c[8]), (double)c[22] / std::max(1ull, c[8]));
+    if (c[14] > 0)
+        std::fprintf(stderr, "[pt] SHADE cycles/iteration: shading %.0f tasks %.0f new-path %.0f ray-start %.0f\n",
+                     (double)c[16] / std::max(1ull, c[10]), (double)c[17] / std::max(1ull, c[10]),
+                     (double)c[18] / std::max(1ull, c[10]), (double)c[19] / std::max(1ull, c[10]));
+}
+
+// The film's last render -> pt_stats: waits for its counters (copied to pinned memory in stream
+// order, event ev2) and takes the kernels' time from its events; reports a tripped traversal guard.
+int filmStats(pt_film* f, pt_stats* stats) {
+    if (!f->rendered) return fail(PT_ERR_STATE, "pt_film_stats: no render on this film yet");
+    HIP_TRY(hipEventSynchronize(f->ev2));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, f->ev0, f->ev1));
+    const unsigned long long* c = f->hostCounters;
+    fillStats(stats, c, ms, f->lastWide);
+    if (std::getenv("PT_ITER_STATS")) printIterStats(c, f->lastWide);
+    if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
+    return PT_OK;
 }
 }  // namespace
 
@@ -2522,7 +2656,9 @@ int pt_scene_update_objects(pt_scene* s, const pt_object* objs, int64_t first, i
     return PT_OK;
 }
 
-int pt_scene_build_bvh(pt_scene* s, int flags) {
+int pt_scene_build_bvh(pt_scene* s, int flags) { return pt_scene_build_bvh_ex(s, flags, nullptr); }
+
+int pt_scene_build_bvh_ex(pt_scene* s, int flags, void* stream) {
     if (!s) return fail(PT_ERR_INVALID, "pt_scene_build_bvh: null scene");
     int rc = setDevice(s->device);
     if (rc) return rc;
@@ -2548,10 +2684,13 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
         (rc = devReserve(ids2, n1 * 4)) || (rc = devReserve(box6, (1 + kBoxBlocks) * 6 * sizeof(float))) || (rc = devReserve(sph, n1 * 4)) ||
         (rc = devReserve(arr, ni * 4)) || (rc = devReserve(dep, 16)))
         return rc;
-    hipStream_t st = 0;
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // Every return path destroys the events and, on failure, waits for the work already queued on
+    // the stream (it uses the scene's buffers).
+    StreamGuard guard(st);
+    HIP_TRY(hipEventCreate(&guard.e0));
+    HIP_TRY(hipEventCreate(&guard.e1));
+    hipEvent_t e0 = guard.e0, e1 = guard.e1;
     HIP_TRY(hipEventRecord(e0, st));
     const unsigned tb = 256, nb = (unsigned)((n1 + tb - 1) / tb), nbi = (unsigned)((ni + tb - 1) / tb);
     if (n > 0) {
@@ -2611,14 +2750,34 @@ int pt_scene_build_bvh(pt_scene* s, int flags) {
     }
     HIP_TRY(hipEventRecord(e1, st));
     HIP_TRY(hipEventSynchronize(e1));
+    guard.ok = true;
     float ms = 0.0f;
     HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     s->buildMs = ms;
     int depth = 0;
     HIP_TRY(hipMemcpy(&depth, dep.p, 4, hipMemcpyDeviceToHost));
     s->depth = n > 1 ? depth : 0;
+    if (n > 0) {   // the tight scene box: union of the root's child boxes (a single object: its box)
+        float mn[3], mx[3];
+        if (n > 1) {
+            float r[12];
+            HIP_TRY(hipMemcpy(r, s->nodes.p, sizeof(r), hipMemcpyDeviceToHost));
+            for (int a = 0; a < 3; a++) {
+                mn[a] = std::fmin(r[nodeBoxIdx(0, a, 0)], r[nodeBoxIdx(1, a, 0)]);
+                mx[a] = std::fmax(r[nodeBoxIdx(0, a, 1)], r[nodeBoxIdx(1, a, 1)]);
+            }
+        } else {
+            float b6[6];
+            HIP_TRY(hipMemcpy(b6, s->leafBoxes.p, sizeof(b6), hipMemcpyDeviceToHost));
+            for (int a = 0; a < 3; a++) { mn[a] = b6[a]; mx[a] = b6[3 + a]; }
+        }
+        float e = 0.0f;
+        for (int a = 0; a < 3; a++) {
+            s->sceneCE[a] = 0.5f * (mn[a] + mx[a]);
+            e = std::fmax(e, mx[a] - mn[a]);
+        }
+        s->sceneCE[3] = e;
+    }
     if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
     if (s->wideReady && wideStackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");
     s->deviceBytes = (size_t)(n > 1 ? n - 1 : 0) * 64 + (size_t)n * 96 + (size_t)s->nmat * 32;
@@ -2743,21 +2902,18 @@ int traceDevice(pt_scene* s, const pt_ray* dr, int64_t n, float tmin, float tmax
     const bool wide = kernel == PT_KERNEL_WIDE;
     if (wide && (rc = ensureWide(s))) return rc;
     const int stack = wide ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
+    StreamGuard guard(st);
     HIP_TRY(hipMemsetAsync(s->counters.p, 0, kNumCounters * sizeof(unsigned long long), st));
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, st));
-    if (n > 0 && (rc = dispatchTrace(stack, wide, devScene(s), dr, n, tmin, tmax, dh, s->counters.as<unsigned long long>(), st))) {
-        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    HIP_TRY(hipEventCreate(&guard.e0));
+    HIP_TRY(hipEventCreate(&guard.e1));
+    HIP_TRY(hipEventRecord(guard.e0, st));
+    if (n > 0 && (rc = dispatchTrace(stack, wide, devScene(s), dr, n, tmin, tmax, dh, s->counters.as<unsigned long long>(), st)))
         return rc;
-    }
-    HIP_TRY(hipEventRecord(e1, st));
-    HIP_TRY(hipEventSynchronize(e1));
+    HIP_TRY(hipEventRecord(guard.e1, st));
+    HIP_TRY(hipEventSynchronize(guard.e1));
+    guard.ok = true;
     float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    HIP_TRY(hipEventElapsedTime(&ms, guard.e0, guard.e1));
     unsigned long long c[kNumCounters] = {0};
     HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
     c[4] = 0;
@@ -2902,15 +3058,39 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     const size_t outBpp = fmt == PT_OUT_RGB32F ? 12 : 4;
     if (accumulate && f->accumSamples + spp >= (1ll << 24))
         return fail(PT_ERR_INVALID, "pt_render_ex: accumulated samples must stay below 2^24");
-    DevBuf dout;
+    // Kernel choice and wavefront-scheduler thresholds (lanes of 64): explicit options win, then
+    // the PT_RENDER_KERNEL / PT_LEAF_BATCH / PT_SHADE_BATCH environment (tuning), then defaults.
+    int kernel = opts ? opts->kernel : PT_KERNEL_DEFAULT;
+    if (kernel == PT_KERNEL_DEFAULT) {
+        const char* k = std::getenv("PT_RENDER_KERNEL");
+        const std::string ks = k ? k : "";
+        kernel = ks == "simple" ? PT_KERNEL_SIMPLE : (ks == "wavefront" ? PT_KERNEL_WAVEFRONT : PT_KERNEL_WIDE);
+    }
+    if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
+        return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
+    const int rng = opts ? opts->rng : PT_RNG_COMPAT;
+    if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
+    if (kernel == PT_KERNEL_WIDE && (rc = ensureWide(s))) return rc;   // (first use: builds the tree)
+
+    // Film resources, allocated once and reused by every later render (no hipMalloc / hipFree,
+    // which synchronise the device, in the per-frame path).
+    if (!f->ev0) {
+        HIP_TRY(hipEventCreate(&f->ev0));
+        HIP_TRY(hipEventCreate(&f->ev1));
+        HIP_TRY(hipEventCreateWithFlags(&f->ev2, hipEventDisableTiming));
+    }
+    if (!f->counters.p && (rc = devAlloc(f->counters, kNumCounters * sizeof(unsigned long long)))) return rc;
+    if (!f->hostCounters) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&f->hostCounters),
+                                                kNumCounters * sizeof(unsigned long long), hipHostMallocDefault));
     void* dst = out;
     if (!on_dev) {
-        if ((rc = devAlloc(dout, (size_t)std::max<int64_t>(1, np) * outBpp))) return rc;
-        dst = dout.p;
+        if ((rc = devReserve(f->staging, (size_t)std::max<int64_t>(1, np) * outBpp))) return rc;
+        dst = f->staging.p;
     }
-    HIP_TRY(hipMemsetAsync(s->counters.p, 0, kNumCounters * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(f->counters.p, 0, kNumCounters * sizeof(unsigned long long), st));
     RenderParams P;
     P.S = devScene(s);
+    P.S.err = reinterpret_cast<unsigned int*>(f->counters.as<unsigned long long>() + 7);
     P.cam.pos = make_float3(cam->origin[0], cam->origin[1], cam->origin[2]);
     P.cam.ll = make_float3(cam->lower_left[0], cam->lower_left[1], cam->lower_left[2]);
     P.cam.hor = make_float3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
@@ -2920,7 +3100,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.out = static_cast<float*>(dst);
     P.rawOut = 0;
     P.sampleBase = 0;
-    P.counters = s->counters.as<unsigned long long>();
+    P.counters = f->counters.as<unsigned long long>();
     P.width = f->width;
     P.nrows = f->nrows;
     P.stripe_h = f->stripe_h;
@@ -2934,40 +3114,21 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.invW = 1.0f / (float)f->width;    // main.cu:281
     P.invH = 1.0f / (float)f->height;
     P.invSpp = 1.0f / (float)spp;
-    // Kernel choice and wavefront-scheduler thresholds (lanes of 64): explicit options win, then
-    // the PT_RENDER_KERNEL / PT_LEAF_BATCH / PT_SHADE_BATCH environment (tuning), then defaults.
-    int kernel = opts ? opts->kernel : PT_KERNEL_DEFAULT;
-    if (kernel == PT_KERNEL_DEFAULT) {
-        const char* k = std::getenv("PT_RENDER_KERNEL");
-        const std::string ks = k ? k : "";
-        kernel = ks == "simple" ? PT_KERNEL_SIMPLE : (ks == "wavefront" ? PT_KERNEL_WAVEFRONT : PT_KERNEL_WIDE);
-    }
-    if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
-        return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
-
-    const int rng = opts ? opts->rng : PT_RNG_COMPAT;
-    if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
-
-    if (kernel == PT_KERNEL_WIDE) {
-        if ((rc = ensureWide(s))) return rc;
-        P.S = devScene(s);   // now with the wide nodes
-        if (s->nobj > 0 && (!P.S.wnodes || !P.S.wprims)) return fail(PT_ERR_STATE, "wide BVH missing");
-    }
+    if (kernel == PT_KERNEL_WIDE && s->nobj > 0 && (!P.S.wnodes || !P.S.wprims)) return fail(PT_ERR_STATE, "wide BVH missing");
     P.kernel = kernel;
     P.nblocks = 0;
     P.block = 0;
     P.blockShift = -1;
-    P.partial = nullptr;
+    P.pixAcc = nullptr;
     P.taskCounter = nullptr;
     P.stackSpill = nullptr;
     P.ntasks = 0;
     P.nwaves = 0;
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
-    // Defaults swept on C3 (tools/gpu_variants.sh): sample mode is throughput-bound and prefers
-    // full LEAF / SHADE steps (24 / 32: 1,741 -> 1,326..1,355 ms when introduced).  Compat mode
-    // is bound by its slowest pixels' sequential chains: 20 / 12 together with nodeMin 8 (C3
-    // 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 -> 1,180 against 8 / 12).
+    // Defaults swept on C3 (tools/ab_env.py): sample mode is throughput-bound and prefers full
+    // LEAF / SHADE steps.  Compat mode is bound by its slowest pixels' sequential chains: 20 / 12
+    // together with nodeMin 8 (C3 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 -> 1,180 against 8 / 12).
     const bool sampleRng = rng == PT_RNG_SAMPLE;
     // sample mode, wide kernel (speculative traversal): LEAF at 28 waiting lanes, SHADE at 28
     // (C3 @256 spp 148.4 -> 145.0 ms vs 24 / 32; C5 @64 75.9 -> 74.5; C2 @1024 135.4 -> 134.5)
@@ -2994,12 +3155,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         P.block = (opts && opts->chunk > 0) ? opts->chunk : std::max(16, (spp + 63) / 64);
         P.nblocks = (spp + P.block - 1) / P.block;
         P.blockShift = (P.block & (P.block - 1)) == 0 ? __builtin_ctz((unsigned)P.block) : -1;
-        const size_t need = (size_t)P.nblocks * (size_t)np * 16;   // {block sum xyz, rays}
-        if (f->partialBytes < need) {
-            if ((rc = devAlloc(f->partial, need))) return rc;
-            f->partialBytes = need;
-        }
-        P.partial = f->partial.as<float>();
+        if ((rc = devReserve(f->pixAcc, (size_t)np * 32))) return rc;   // {x, y, z, rays} per pixel
+        HIP_TRY(hipMemsetAsync(f->pixAcc.p, 0, (size_t)np * 32, st));
+        P.pixAcc = f->pixAcc.as<unsigned long long>();
         const uint64_t ntasks = (uint64_t)P.ntiles * (uint64_t)P.nblocks * 64u;
         if (ntasks >= (1ull << 32) - 4096)
             return fail(PT_ERR_INVALID, "sample mode: too many (pixel, block) tasks; raise the block size (chunk)");
@@ -3018,7 +3176,6 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
-
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
     }
     // Deep trees: stack entries beyond kLdsStack live in memory, per wave slot (persistent wave or
@@ -3056,18 +3213,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         HIP_TRY(hipMemsetAsync(dtimes.p, 0, nwaves * 24, st));
         P.waveTimes = dtimes.as<unsigned long long>();
     }
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, st));
-    if (P.ntiles > 0 && (rc = dispatchRender(stack, P, st))) {
-        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
-        return rc;
-    }
+    // From here on the film describes this render (pt_film_stats reads it).
+    f->rendered = false;
+    f->lastWide = kernel == PT_KERNEL_WIDE;
+    HIP_TRY(hipEventRecord(f->ev0, st));
+    if (P.ntiles > 0 && (rc = dispatchRender(stack, P, st))) return rc;
     if (resolve) {
         const float inv = accumulate ? 1.0f / (float)(f->accumSamples + spp) : P.invSpp;
-        resolveKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(sample ? P.partial : f->sums.as<float>(),
-                                                                     sample ? P.nblocks : 0,
+        resolveKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(f->sums.as<float>(), sample ? P.pixAcc : nullptr,
                                                                      accumulate ? f->accum.as<float>() : nullptr,
                                                                      inv, fmt, dst, np,
                                                                      sample ? f->tileCost.as<unsigned>() : nullptr,
@@ -3075,24 +3228,30 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         HIP_TRY(hipGetLastError());
     }
     if (accumulate) f->accumSamples += spp;
-    HIP_TRY(hipEventRecord(e1, st));
-    HIP_TRY(hipEventSynchronize(e1));
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (lpt && P.ntiles > 0) {   // next launch: longest tiles first
-        std::vector<unsigned>& cost = f->cost;
-        cost.resize(ntl);
-        HIP_TRY(hipMemcpy(cost.data(), f->tileCost.p, ntl * 4, hipMemcpyDeviceToHost));
-        f->costSpp = spp;
-        std::vector<int> order(ntl);
-        for (size_t i = 0; i < ntl; i++) order[i] = (int)i;
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
-        HIP_TRY(hipMemcpy(f->tileOrder.p, order.data(), ntl * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipEventRecord(f->ev1, st));
+    // the counters to pinned host memory, in stream order (pt_film_stats waits for ev2 only)
+    HIP_TRY(hipMemcpyAsync(f->hostCounters, f->counters.p, kNumCounters * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(f->ev2, st));
+    f->rendered = true;
+    if (lpt && P.ntiles > 0) {   // next launch: longest tiles first (a stable radix sort, on the device)
+        const int nt = (int)ntl;
+        if ((rc = devReserve(f->tileKeys, ntl * 4)) || (rc = devReserve(f->tileKeys2, ntl * 4)) ||
+            (rc = devReserve(f->tileIds, ntl * 4)))
+            return rc;
+        size_t tbytes = 0;
+        HIP_TRY(pt::radixSortPairs(nullptr, &tbytes, f->tileKeys.as<uint32_t>(), f->tileKeys2.as<uint32_t>(),
+                                   f->tileIds.as<uint32_t>(), f->tileOrder.as<uint32_t>(), ntl, 32, st));
+        if ((rc = devReserve(f->sortTemp, tbytes))) return rc;
+        tileKeyKernel<<<(unsigned)((nt + 255) / 256), 256, 0, st>>>(f->tileCost.as<unsigned>(), f->tileKeys.as<uint32_t>(),
+                                                                    f->tileIds.as<uint32_t>(), nt);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(pt::radixSortPairs(f->sortTemp.p, &tbytes, f->tileKeys.as<uint32_t>(), f->tileKeys2.as<uint32_t>(),
+                                   f->tileIds.as<uint32_t>(), f->tileOrder.as<uint32_t>(), ntl, 32, st));
         f->haveOrder = true;
     }
     if (P.waveTimes) {
+        HIP_TRY(hipStreamSynchronize(st));
         std::vector<unsigned long long> t(nwaves * 3);
         HIP_TRY(hipMemcpy(t.data(), dtimes.p, t.size() * 8, hipMemcpyDeviceToHost));
         if (FILE* fp = std::fopen(timesPath, "wb")) {
@@ -3101,28 +3260,16 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         }
     }
     if (!on_dev && np > 0) HIP_TRY(hipMemcpy(out, dst, np * outBpp, hipMemcpyDeviceToHost));
-    unsigned long long c[kNumCounters] = {0};
-    HIP_TRY(hipMemcpy(c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
-    fillStats(stats, c, ms, kernel == PT_KERNEL_WIDE);
-    if (std::getenv("PT_ITER_STATS") && c[8] + c[9] + c[10] > 0)   // diagnostic: wavefront scheduler
-        std::fprintf(stderr, "[pt] iterations node %llu leaf %llu shade %llu | lanes/iter node %.1f leaf %.1f "
-                     "shade %.1f\n", c[8], c[9], c[10], (double)c[1] / std::max(1ull, c[8]),
-                     (double)c[11] / std::max(1ull, c[9]), (double)c[0] / std::max(1ull, c[10]));
-    if (std::getenv("PT_ITER_STATS") && c[12] + c[13] + c[14] > 0)
-        std::fprintf(stderr, "[pt] cycles/iteration node %.0f leaf %.0f shade %.0f | share node %.3f leaf %.3f "
-                     "shade %.3f\n", (double)c[12] / std::max(1ull, c[8]), (double)c[13] / std::max(1ull, c[9]),
-                     (double)c[14] / std::max(1ull, c[10]), (double)c[12] / (double)(c[12] + c[13] + c[14]),
-                     (double)c[13] / (double)(c[12] + c[13] + c[14]), (double)c[14] / (double)(c[12] + c[13] + c[14]));
-    if (std::getenv("PT_ITER_STATS") && kernel == PT_KERNEL_WIDE)
-        std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps); NODE steps: "
-                     "lanes waiting on primitives with nodes left %.1f, lanes without NODE work %.1f\n", c[20],
-                     (double)c[21] / std::max(1ull, c[8]), (double)c[22] / std::max(1ull, c[8]));
-    if (std::getenv("PT_ITER_STATS") && c[14] > 0)
-        std::fprintf(stderr, "[pt] SHADE cycles/iteration: shading %.0f tasks %.0f new-path %.0f ray-start %.0f\n",
-                     (double)c[16] / std::max(1ull, c[10]), (double)c[17] / std::max(1ull, c[10]),
-                     (double)c[18] / std::max(1ull, c[10]), (double)c[19] / std::max(1ull, c[10]));
-    if (c[7]) return fail(PT_ERR_STATE, "traversal guard tripped (corrupt BVH), flags " + std::to_string(c[7]));
+    // With stats (or a host output) the call waits for the frame; without, it returns at once.
+    if (stats || !on_dev) return filmStats(f, stats);
     return PT_OK;
+}
+
+int pt_film_stats(pt_film* f, pt_stats* stats) {
+    if (!f || !stats) return fail(PT_ERR_INVALID, "pt_film_stats: null argument");
+    int rc = setDevice(f->device);
+    if (rc) return rc;
+    return filmStats(f, stats);
 }
 
 void pt_film_destroy(pt_film* f) {

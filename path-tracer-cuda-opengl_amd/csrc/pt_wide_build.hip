@@ -380,7 +380,7 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
         atomicOr(misc + kMiscErr, 1u);
         return;
     }
-    // smallest plane quantum: 2^-20 of the scene extent (the host build's rule)
+    // smallest plane quantum: 2^-18 of the scene extent (the host build's rule, pt_wide8.cpp)
     const uint32_t root = *rootCid;
     const float4 rlo = T.pbox[2 * (size_t)root], rhi = T.pbox[2 * (size_t)root + 1];
     double ext = 0.0;
@@ -389,7 +389,7 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
         for (int a = 0; a < 3; a++)
             ext = fmax(ext, fmax(fabs((double)l[a]), fmax(fabs((double)h[a]), (double)h[a] - (double)l[a])));
     }
-    int emin = ext > 0.0 ? ceilLog2(ext) - 20 : -100;
+    int emin = ext > 0.0 ? ceilLog2(ext) - 18 : -100;
     emin = emin < -100 ? -100 : emin;
 
     float cmn[8][3], cmx[8][3];
@@ -653,7 +653,7 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
 
     // 3. collapse + quantisation, level by level
     const Tree T{pbox, pchild, (uint32_t)n};
-    const uint32_t slotCap = (uint32_t)wideDevNodeSlots(n);
+    const uint32_t slotCap = wideDevSlotCap(n);   // <= 2^24: child bases fit the kernels' 24-bit field
     setRootKernel<<<1, 1, 0, st>>>(rootCid, static_cast<uint2*>(items_[0].p));
     WB_TRY(hipGetLastError());
     int it = 0;

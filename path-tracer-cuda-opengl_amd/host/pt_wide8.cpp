@@ -244,12 +244,14 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
     const BBox rootBox = B.nodes[root].box;
 
     // Smallest plane quantum: far below any box of interest, far above the rounding of the
-    // ray arithmetic (|p - o| * inv with |p - o| up to a few scene extents): 2^-20 of the scene.
+    // ray arithmetic (|p - o| * inv: about 2^-21.6 |p - o|, for origins within 8 scene extents of
+    // the centre -- farther ones are traced in the reference's order, pt_device.hip wideFar):
+    // 2^-18 of the larger of the scene's extent and coordinates.
     double ext = 0.0;
     for (int a = 0; a < 3; a++)
         ext = std::max({ext, std::fabs((double)rootBox.mn[a]), std::fabs((double)rootBox.mx[a]),
                         (double)rootBox.mx[a] - (double)rootBox.mn[a]});
-    int emin = ext > 0.0 ? (int)std::ceil(std::log2(ext)) - 20 : -100;
+    int emin = ext > 0.0 ? (int)std::ceil(std::log2(ext)) - 18 : -100;
     emin = std::max(emin, -100);
 
     const char* sl = std::getenv("PT_WIDE_SPLIT_LEAVES");

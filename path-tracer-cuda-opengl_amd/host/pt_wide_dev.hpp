@@ -39,6 +39,14 @@ struct WideDevOut {
 // Node slots the device build may use: a node with a child block has 8 children and consumes 7
 // internal nodes of the binary tree, so at most 1 + 8 * floor((n - 1) / 7) slots.
 inline int64_t wideDevNodeSlots(int64_t n) { return 1 + 8 * ((n > 1 ? n - 1 : 0) / 7 + 1); }
+// The traversal kernels carry a node's child base in 24 bits (ng = childBase << 8 | hit slots), so
+// a child block must end at or below 2^24 slots: the build reports an error instead of writing a
+// base that would be truncated (host build: pt_wide8.cpp checks the same limit).
+constexpr int64_t kWideMaxSlots = (int64_t)1 << 24;
+inline uint32_t wideDevSlotCap(int64_t n) {
+    const int64_t s = wideDevNodeSlots(n);
+    return (uint32_t)(s < kWideMaxSlots ? s : kWideMaxSlots);
+}
 
 class WideDevBuilder {
 public:

@@ -78,6 +78,7 @@ EXPORTS = [
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
     "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
     "pt_scene_update_objects", "pt_trace_closest_ex", "pt_scene_wide_info", "pt_trace_closest_device",
+    "pt_scene_build_bvh_ex", "pt_film_stats",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -101,6 +102,8 @@ _sig = {
     "pt_quantize_rgba8": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "pt_scene_create": (C.c_int, [C.c_int, _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_void_p)]),
     "pt_scene_build_bvh": (C.c_int, [_P, C.c_int]),
+    "pt_scene_build_bvh_ex": (C.c_int, [_P, C.c_int, _P]),
+    "pt_film_stats": (C.c_int, [_P, C.POINTER(Stats)]),
     "pt_scene_build_time": (C.c_int, [_P, C.POINTER(C.c_double)]),
     "pt_scene_update_objects": (C.c_int, [_P, _P, C.c_int64, C.c_int64]),
     "pt_scene_bvh_info": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -246,8 +249,10 @@ class Scene:
         if build:
             self.build_bvh(flags)
 
-    def build_bvh(self, flags: int = PT_BVH_ORIGIN_BOUNDS) -> None:
-        _check(lib.pt_scene_build_bvh(self.h, flags), "pt_scene_build_bvh")
+    def build_bvh(self, flags: int = PT_BVH_ORIGIN_BOUNDS, stream=None) -> None:
+        """pt_scene_build_bvh_ex: the build's device work on `stream` (a hipStream_t handle or None)."""
+        _check(lib.pt_scene_build_bvh_ex(self.h, flags, C.c_void_p(int(stream) if stream else 0)),
+               "pt_scene_build_bvh_ex")
 
     def update_objects(self, objects: np.ndarray, first: int = 0) -> None:
         """Overwrite objects [first, first + len(objects)); the BVH must be rebuilt (build_bvh)
@@ -348,6 +353,12 @@ class Film:
         """Progressive rendering: restart the accumulation (e.g. after the camera moved)."""
         _check(lib.pt_film_clear(self.h, C.c_void_p(int(stream) if stream else 0)), "pt_film_clear")
 
+    def stats(self) -> "Stats":
+        """pt_film_stats: counters and kernel time of the last render (waits for it)."""
+        st = Stats()
+        _check(lib.pt_film_stats(self.h, C.byref(st)), "pt_film_stats")
+        return st
+
     @property
     def accumulated(self) -> int:
         n = C.c_int64()
@@ -368,11 +379,14 @@ class Film:
 
 def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, out=None, stream=None,
            kernel: int = KERNEL_DEFAULT, leaf_batch: int = 0, shade_batch: int = 0, rng: int = RNG_COMPAT,
-           chunk: int = 0, flags: int = 0, accumulate: bool = False, out_format: int = OUT_RGB32F):
+           chunk: int = 0, flags: int = 0, accumulate: bool = False, out_format: int = OUT_RGB32F,
+           wait: bool = True):
     """Render spp samples per pixel of the film's rows.  `out` may be a numpy array (host) or
     an integer device pointer (then `stream` is a hipStream_t handle or None).  Returns
     (rgb or None, Stats); rgb is float32 (n_pixels, 3), or uint8 (n_pixels, 4) for the 8-bit
-    output formats.  accumulate=True adds the frame to the film's running sums (progressive)."""
+    output formats.  accumulate=True adds the frame to the film's running sums (progressive).
+    wait=False (device output only): the frame is enqueued and the call returns at once with
+    Stats None -- film.stats() waits for it and returns its counters."""
     st = Stats()
     if accumulate:
         flags |= ACCUMULATE
@@ -389,5 +403,6 @@ def render(scene: Scene, film: Film, camera: Camera, spp: int, max_depth: int, o
                                 C.byref(st)), "pt_render_ex")
         return rgb, st
     _check(lib.pt_render_ex(scene.h, film.h, C.byref(camera), spp, max_depth, C.c_void_p(int(out)), 1,
-                            C.c_void_p(int(stream) if stream else 0), C.byref(opts), C.byref(st)), "pt_render_ex")
-    return None, st
+                            C.c_void_p(int(stream) if stream else 0), C.byref(opts), C.byref(st) if wait else None),
+           "pt_render_ex")
+    return None, (st if wait else None)

@@ -1,4 +1,4 @@
-"""Multi-rank path on CPU (gloo, world_size 2 and 3): stripe partition + all-gather +
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): stripe partition + gather to rank 0 +
 un-permute reproduce the single-rank frame bit-exactly.  The per-rank render here is the
 oracle (CPU); on the GPU box bench.py runs the same partition with libpt.so and RCCL."""
 import os
@@ -44,8 +44,7 @@ def _worker(rank, world, port, w, h, stripe, spp, q, rgba8=False):
         px = rgb
         buf = torch.zeros((mr * w * 3,), dtype=torch.float32)      # flat
     buf[: px.size] = torch.from_numpy(px.reshape(-1))
-    out = torch.empty((world * buf.numel(),), dtype=buf.dtype)
-    dist.all_gather_into_tensor(out, buf)
+    out = ptdist.gather_to_root(buf, world, rank)
     total = torch.tensor([float(st.rays)], dtype=torch.float64)
     dist.all_reduce(total)
     if rank == 0:
@@ -55,7 +54,7 @@ def _worker(rank, world, port, w, h, stripe, spp, q, rgba8=False):
 
 
 @pytest.mark.parametrize("world,stripe,rgba8", [(2, 8, False), (3, 5, False), (2, 4, True)])
-def test_stripes_allgather_equals_single_rank(world, stripe, rgba8):
+def test_stripes_gather_equals_single_rank(world, stripe, rgba8):
     sys.path[:0] = [os.path.join(REPO, "path-tracer-cuda-opengl_amd", "python"), os.path.join(REPO, "oracle")]
     import oracle
     import ptamd

@@ -198,3 +198,49 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
                         common[1:] + ["--png", two], cwd=repo, capture_output=True, text=True, timeout=300, env=env)
     assert r2.returncode == 0, r2.stderr[-2000:]
     np.testing.assert_array_equal(read_png(one), read_png(two))
+
+
+@pytest.mark.parametrize("rng", ["compat", "sample"])
+def test_async_frames_match_synchronous(pt, setup, rng):
+    """pt_render_ex with a device output and no pt_stats returns before the frame is done
+    (interactive use: camera move, clear, accumulate, display, next frame); pt_film_stats then
+    waits for the film's last frame.  Queued frames give the same images and counters as the same
+    frames rendered one at a time."""
+    import torch
+    p, scene, _, _ = setup
+    r = pt.RNG_COMPAT if rng == "compat" else pt.RNG_SAMPLE
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    cams = []
+    cam = pt.Camera.from_buffer_copy(bytes(p.camera))
+    for k in range(4):
+        pt.camera_move(cam, k % 6, 0.05)
+        cams.append(pt.Camera.from_buffer_copy(bytes(cam)))
+
+    def frames(wait):
+        film = pt.Film(W, H, seed=7)
+        outs, stats = [], []
+        for c in cams:
+            buf = torch.zeros(W * H * 4, dtype=torch.uint8, device=dev)
+            film.clear(stream.cuda_stream)
+            _, st = pt.render(scene, film, c, 3, DEPTH, out=buf.data_ptr(), stream=stream.cuda_stream, rng=r,
+                              accumulate=True, out_format=pt.OUT_RGBA8_SURFACE, wait=wait)
+            if not wait:
+                assert st is None
+                st = film.stats()   # waits for this frame only
+            outs.append(buf)
+            stats.append((st.rays, st.paths, st.node_visits))
+        torch.cuda.synchronize(dev)
+        return [o.cpu().numpy() for o in outs], stats
+
+    a, sa = frames(True)
+    b, sb = frames(False)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    assert sa == sb and all(s[1] == W * H * 3 for s in sa)
+
+
+def test_film_stats_before_any_render_fails(pt, gpu):
+    film = pt.Film(8, 8, seed=1, device=gpu)
+    with pytest.raises(pt.PtError):
+        film.stats()

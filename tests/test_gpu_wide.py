@@ -256,3 +256,46 @@ def test_trace_device_pointers_match_host_api(pt, orc, gpu, wb):
         got = hd.cpu().numpy().view(pt.HIT_DTYPE)
         assert_hits_equal(got, want)
         assert (st.rays, st.node_visits, st.tri_tests) == (wst.rays, wst.node_visits, wst.tri_tests)
+
+
+@pytest.mark.parametrize("dist", [3.0, 7.5, 100.0, 1000.0])
+def test_wide_trace_far_origins(pt, orc, gpu, wb, dist):
+    """the wide boxes' one-quantum margin covers the rounding of the plane distances
+    only for origins within about 11 scene extents; origins beyond 8 extents from the scene's
+    centre are traced in the reference's order (wideFar).  Rays from `dist` extents away, aimed at
+    the scene's primitives (many graze edges and corners of small nodes), must keep the
+    reference's hits either way."""
+    p = pt.Preset("bunny_cornell", 64, 36)
+    objs = p.objects
+    lo = objs["v"][:, :3].min(0)
+    hi = objs["v"][:, :3].max(0)
+    ext = float((hi - lo).max())
+    rays = random_rays(8192, seed=int(dist) + 21, center=(lo + hi) / 2, radius=dist * ext, objects=objs)
+    # aim half of the rays at triangle vertices and edge midpoints: grazing hits on tiny boxes
+    rng = np.random.default_rng(int(dist))
+    k = rng.integers(0, len(objs), 4096)
+    v = objs["v"][k].reshape(-1, 3, 3)
+    j = rng.integers(0, 3, 4096)
+    tgt = np.where((np.arange(4096) % 2 == 0)[:, None], v[np.arange(4096), j],
+                   0.5 * (v[np.arange(4096), j] + v[np.arange(4096), (j + 1) % 3]))
+    rays[4096:, 3:] = (tgt - rays[4096:, :3]).astype(np.float32)
+    hits, st, ref, rst = trace_both(pt, orc, gpu, wb, objs, p.materials, rays)
+    assert_hits_equal(hits, ref)
+    assert ref["hit"].sum() > 4000
+    assert st.rays == len(rays)
+
+
+def test_wide_render_far_camera(pt, orc, gpu, wb):
+    """A camera 20 scene extents from the Cornell box (narrow field of view): its camera rays take
+    the reference-order path, the bounces inside the box the wide tree; frame bit-exact."""
+    p = pt.Preset("cornell", 48, 48)
+    w, h = 48, 48
+    cam = pt.camera_make((278.0, 273.0, -800.0 - 20 * 556.0), (278.0, 273.0, 0.0), 2.0, 1.0)
+    s = make_scene(pt, p.objects, p.materials, gpu, wb)
+    f = pt.Film(w, h, 3, device=gpu)
+    rgb, st = pt.render(s, f, cam, 4, 8, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE, chunk=2)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    ref, rst = orc.render_sample(p.objects, p.materials, nodes, pt.camera_to_array(cam), w, h, f.rows, 4, 8, 3, 2,
+                                 nthreads=8)
+    assert np.array_equal(bits(rgb), bits(ref))
+    assert st.rays == rst.rays and st.rays > w * h * 4

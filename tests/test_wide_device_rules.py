@@ -156,3 +156,17 @@ def test_ploc_equal_boxes_halve_per_pass():
         assert merged == before // 2
         passes += 1
     assert passes == int(np.ceil(np.log2(m)))
+
+
+def test_device_build_child_bases_fit_24_bits(tmp_path):
+    """the device build caps its node slots at 2^24 (pt_wide_dev.hpp wideDevSlotCap),
+    so a child base the kernels truncate to 24 bits is reported as an error, never written."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "wide_dev_limits")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I" + os.path.join(root, "path-tracer-cuda-opengl_amd", "host"),
+                    os.path.join(root, "tests", "cpp", "wide_dev_limits.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr

@@ -1,6 +1,7 @@
 """Copy a tools/profile.sh run (gpurun_out/<TAG>/) into profiles/<TAG>/ and derive the per-launch
-HBM traffic of the sample-mode render kernel from the PMC passes -> profiles/traffic.json (read by
-bench.py for `roofline.traffic`).
+HBM traffic of the sample-mode render kernel from the PMC passes -> an entry of profiles/traffic.json
+(read by bench.py for `roofline.traffic`), keyed by workload, spp, RNG mode, kernel and the
+build id (sha256 of libpt.so) the run measured: bench.py reports the counters only for that build.
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 reports both in KiB; on gfx950
 FETCH_SIZE counts half of the bytes of 128-B requests, MI355X_MICROARCH.md "HBM"), taken from the
@@ -54,8 +55,16 @@ def main(tag):
         "source": f"profiles/{tag}/pmc_fetch.csv + pmc_write.csv (separate rocprofv3 --pmc passes; "
                   "2 x FETCH_SIZE + WRITE_SIZE, KiB -> B)",
     }
-    with open(os.path.join(REPO, "profiles", "traffic.json"), "w") as f:
-        json.dump(out, f, indent=1)
+    out["build_id"] = bench["build_id"]
+    # TCC (L2) hits and misses of the same launch, when that pass ran: is the tree L2-resident?
+    tcc_csv = os.path.join(dst, "pmc_tcc.csv")
+    if os.path.exists(tcc_csv):
+        hit = [v for k, v in render_launches(tcc_csv, "TCC_HIT_sum") if "renderKernelWF" in k]
+        miss = [v for k, v in render_launches(tcc_csv, "TCC_MISS_sum") if "renderKernelWF" in k]
+        if hit and miss:
+            out["tcc_hit"], out["tcc_miss"] = hit[-1], miss[-1]
+            out["tcc_hit_rate"] = hit[-1] / max(1.0, hit[-1] + miss[-1])
+    store("traffic", out)
     print(json.dumps(out, indent=1))
     # VALU wave-instructions per launch of the timed (wavefront) render kernel: the wide kernel's
     # binding resource, reported by bench.py as roofline.valu_issue
@@ -66,9 +75,24 @@ def main(tag):
             v = {key: out[key] for key in ("workload", "spp", "rng", "kernel")}
             v["valu_wave_instructions_per_launch"] = valu[-1]
             v["source"] = f"profiles/{tag}/pmc_valu.csv (rocprofv3 --pmc SQ_INSTS_VALU, one frame)"
-            with open(os.path.join(REPO, "profiles", "valu.json"), "w") as f:
-                json.dump(v, f, indent=1)
+            v["build_id"] = bench["build_id"]
+            store("valu", v)
             print(json.dumps(v, indent=1))
+
+
+def store(name, entry):
+    """profiles/<name>.json = {"entries": [...]}: one entry per workload (the newest run replaces
+    the entry of the same workload, spp, RNG mode and kernel)."""
+    path = os.path.join(REPO, "profiles", name + ".json")
+    try:
+        data = json.load(open(path))
+        entries = data.get("entries", [])
+    except (OSError, ValueError):
+        entries = []
+    key = lambda e: (e.get("workload"), e.get("spp"), e.get("rng"), e.get("kernel"))  # noqa: E731
+    entries = [e for e in entries if key(e) != key(entry)] + [entry]
+    with open(path, "w") as f:
+        json.dump({"entries": entries}, f, indent=1)
 
 
 if __name__ == "__main__":
