@@ -51,8 +51,11 @@ hipError_t radixSortPairs(void* temp, size_t* temp_bytes, const uint32_t* codes_
 namespace {
 
 constexpr int kWave = 64;
-#ifndef PT_BUFFER_LOADS
-#define PT_BUFFER_LOADS 0   // primitive/shading records through buffer loads: measured 999 vs 995 ms (off)
+#ifndef PT_AB_NO_ATOMICS
+#define PT_AB_NO_ATOMICS 0
+#endif
+#ifndef PT_AB_NO_FAR
+#define PT_AB_NO_FAR 0
 #endif
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
@@ -160,21 +163,11 @@ struct SlabHit { bool hit; float lo; };
 //   [12] left ref  [13] right ref  [14..15] unused
 __host__ __device__ constexpr int nodeBoxIdx(int child, int axis, int isMax) { return 6 * child + 2 * axis + isMax; }
 
-#ifndef PT_PACKED_SLAB
-#define PT_PACKED_SLAB 1
-#endif
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 // slabLo on a box given as (min, max) pairs per axis (the node record layout).
 __device__ __forceinline__ SlabHit slabPair(v2f X, v2f Y, v2f Z, float3 o, float3 inv, float tmin, float tmax) {
-#if PT_PACKED_SLAB
     const v2f tx = (X - o.x) * inv.x, ty = (Y - o.y) * inv.y, tz = (Z - o.z) * inv.z;
-#else
-    v2f tx, ty, tz;
-    tx.x = (X.x - o.x) * inv.x; tx.y = (X.y - o.x) * inv.x;
-    ty.x = (Y.x - o.y) * inv.y; ty.y = (Y.y - o.y) * inv.y;
-    tz.x = (Z.x - o.z) * inv.z; tz.y = (Z.y - o.z) * inv.z;
-#endif
     float nx = inv.x < 0.0f ? tx.y : tx.x, fx = inv.x < 0.0f ? tx.x : tx.y;
     float ny = inv.y < 0.0f ? ty.y : ty.x, fy = inv.y < 0.0f ? ty.x : ty.y;
     float nz = inv.z < 0.0f ? tz.y : tz.x, fz = inv.z < 0.0f ? tz.x : tz.y;
@@ -238,14 +231,8 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off)
 }
 
 __device__ __forceinline__ Prim loadPrim(const DevScene& S, uint32_t k) {
-#if PT_BUFFER_LOADS
-    const __amdgpu_buffer_rsrc_t r = rawRsrc(S.prims);
-    const uint32_t off = k * 48u;
-    return Prim{bload4(r, off), bload4(r, off + 16u), bload4(r, off + 32u)};
-#else
     const float4* p = S.prims + 3 * (size_t)k;
     return Prim{p[0], p[1], p[2]};
-#endif
 }
 
 // CudaObj::hit (cuda_object.h:44-92): returns the accepted t (> tmin > 0), or -1 on a miss.
@@ -570,14 +557,8 @@ struct HitRec { float3 p, n; int mat, obj; bool front; float4 m0; float ir; int 
 
 __device__ __forceinline__ HitRec makeHitFrom(const float4* shade, int k, float t, float3 o, float3 d) {
     HitRec h;
-#if PT_BUFFER_LOADS
-    const __amdgpu_buffer_rsrc_t rs = rawRsrc(shade);
-    const uint32_t off = (uint32_t)k * 48u;
-    const float4 s0 = bload4(rs, off), s1 = bload4(rs, off + 16u), s2 = bload4(rs, off + 32u);
-#else
     const float4* r = shade + 3 * (size_t)k;
     const float4 s0 = r[0], s1 = r[1], s2 = r[2];
-#endif
     const uint32_t tf = __float_as_uint(s2.y);
     h.p = add(o, scale(t, d));
     float3 outward;
@@ -766,6 +747,8 @@ struct RenderParams {
     int nwaves;                               // persistent waves launched
     uint32_t seed0, seed1;
     uint32_t sampleBase;                      // sample mode: index of the frame's first sample
+    int measureCost;                          // sample mode: count rays per pixel for the tile order
+    int camFar;                               // wide: the camera lies beyond the wide boxes' margin (wideFar)
     int rawOut;                               // compat: store the raw sample sum (resolveKernel follows)
     int stripeShift, blockShift;              // log2(stripe_h), log2(block) when powers of two, else -1
 };
@@ -783,13 +766,15 @@ __device__ __forceinline__ unsigned long long blockFixed(float x) {
     return p < 0.0f ? 0ull - u : u;
 }
 __device__ __forceinline__ float fixedToFloat(unsigned long long a) { return (float)((double)(long long)a * 0x1p-32); }
-// One finished (pixel, block) task: its sum and its ray count (the tile-cost input of the next
-// launch's longest-first order) added to the pixel's accumulator, no-return atomics.
-__device__ __forceinline__ void addBlock(unsigned long long* acc, float3 sum, uint32_t rays) {
+// One finished (pixel, block) task: its sum added to the pixel's accumulator, and -- on frames
+// that measure tile costs (`cost`: the input of the next launches' longest-first order) -- its ray
+// count; no-return atomics (device scope: 4 of them per task cost 5 % of a C3 frame, so the ray
+// counts are taken on one frame in eight).
+__device__ __forceinline__ void addBlock(unsigned long long* acc, float3 sum, uint32_t rays, bool cost) {
     __hip_atomic_fetch_add(acc + 0, blockFixed(sum.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(acc + 1, blockFixed(sum.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(acc + 2, blockFixed(sum.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(acc + 3, (unsigned long long)rays, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cost) __hip_atomic_fetch_add(acc + 3, (unsigned long long)rays, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Compat mode end of a pixel: sqrt(sum / spp) (main.cu:290-293), or the raw sum when a resolve
@@ -873,7 +858,7 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
         auto flush = [&]() {
             if constexpr (SAMPLE) {
                 if (sample % P.block == 0 || sample == P.spp) {
-                    addBlock(P.pixAcc + 4 * idx, sum, c.rays - blockRays0 + 1u);
+                    addBlock(P.pixAcc + 4 * idx, sum, c.rays - blockRays0 + 1u, P.measureCost != 0);
                     blockRays0 = c.rays;
                     sum = f3(0.0f, 0.0f, 0.0f);
                 }
@@ -954,12 +939,6 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #ifndef PT_LEAF_QUEUE_SAMPLE
 #define PT_LEAF_QUEUE_SAMPLE 2   // sample mode, binary tree, STACK <= 32; compat prefers 4 (C3 1774 vs 1959 ms)
 #endif
-#ifndef PT_LEAF_PREFETCH
-#define PT_LEAF_PREFETCH 1
-#endif
-#ifndef PT_NODE_BUFFER_LOADS
-#define PT_NODE_BUFFER_LOADS 1
-#endif
 #ifndef PT_TASK_POOL
 #define PT_TASK_POOL 64
 #endif
@@ -980,11 +959,6 @@ constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves 
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
-#ifndef PT_WIDE_PARK
-#define PT_WIDE_PARK 0   // 1: wide kernels keep the path state in LDS between SHADE steps (80 VGPRs fit at 6 waves;
-                         // C3 @256 spp: 5 waves 172.4 ms, 6 waves 174.6 ms, not parked at 5 waves 166.8 ms)
-#endif
-constexpr int kParkWords = 18;
 #ifndef PT_WIDE_SPEC
 #define PT_WIDE_SPEC 1   // wide kernels: speculative traversal, primitive groups a lane may park while it keeps visiting nodes (0-3)
 #endif
@@ -1036,11 +1010,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // per SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
     constexpr int LS = kLdsStack<STACK, SAMPLE, WIDE>;
     __shared__ uint32_t stk[LS * kWave];
-    // Wide kernels park the lane's path state (RNG, attenuation, sums, sample bookkeeping: only
-    // SHADE steps use them) in LDS between SHADE steps, so NODE / LEAF steps run with the ray and
-    // traversal state alone in registers (6 waves per SIMD without spills).  park[w * 64 + lane].
-    constexpr bool PARK = WIDE && PT_WIDE_PARK;
-    __shared__ uint32_t park[PARK ? kParkWords * kWave : 1];
     // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
     // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
     // marks it) and comes back when the current group is empty.
@@ -1051,6 +1020,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     __shared__ float4 flushSum[SAMPLE ? kWave : 1];
     __shared__ uint32_t flushPix[SAMPLE ? kWave : 1];
     bool flushLane = false;
+    // sample mode: the lane's task {pixel col | local row << 16, next sample, end sample, rays}.
+    // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
+    // in four VGPRs carried through every step.
+    __shared__ uint4 taskState[SAMPLE ? kWave : 1];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1070,10 +1043,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     float fcol = (float)col;
     float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
-#if PT_NODE_BUFFER_LOADS
     // gfx9 buffer resource: base = the node array, raw (stride 0), DATA_FORMAT_32 in dword 3
     const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(WIDE ? (const void*)S.wnodes : (const void*)S.nodes);
-#endif
     uint32_t* my = stk + lane;
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
@@ -1089,10 +1060,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #endif
 
     Xorwow g{};
-    uint32_t cr = 0;     // sample mode: the task's pixel, col | local row << 16 (parking wide kernels: compat too)
     if constexpr (!SAMPLE) {
         if (valid) g = Xorwow{P.sd[idx], P.s0[idx], P.s1[idx], P.s2[idx], P.s3[idx], P.s4[idx]};
-        if constexpr (PARK) cr = (uint32_t)col | ((uint32_t)lrow << 16);
     }
     float3 sum = f3(0.0f, 0.0f, 0.0f), o = f3(0.0f, 0.0f, 0.0f), d = f3(0.0f, 0.0f, 1.0f);
     float3 inv = d, att = f3(1.0f, 1.0f, 1.0f);
@@ -1111,7 +1080,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     float bestLo = 0.0f;
     bool active = false;
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
-    uint32_t taskRays = 0, depthPaths = 0;
+    uint32_t depthPaths = 0;
     bool needTask = SAMPLE;
     uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode: the wave's reserved tasks (uniform)
 
@@ -1120,18 +1089,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #define PT_BEGIN_RAY()                                                                              \
     do {                                                                                          \
         depthLeft--;                                                                              \
-        if constexpr (SAMPLE) taskRays++;                                                         \
+        if constexpr (SAMPLE) {   /* rays per task: only frames that measure tile costs use them */ \
+            if (kargs()->measureCost)                                                             \
+                __hip_atomic_fetch_add(&taskState[lane].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+        }                                                                                         \
         closest = __builtin_inff();                                                               \
         best = -1;                                                                                \
         sp = 0;                                                                                   \
         qn = 0;                                                                                   \
         if constexpr (WIDE) {   /* the root is slot 0 of a virtual node at base 0 */              \
             inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                         \
-            oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);  \
+            const uint32_t oc_ = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u); \
+            oct = oc_;                                                                            \
             tg = 0u;                                                                              \
             bestLo = -__builtin_inff();                                                           \
-            ng = S.nprims > 0 ? (1u << oct) : 0u;                                                 \
-            if (wideFar(kargs()->S.cx, kargs()->S.cy, kargs()->S.cz, kargs()->S.ext, o)) {         \
+            ng = S.nprims > 0 ? (1u << oc_) : 0u;                                                 \
+            /* only camera rays can start far from the scene (a bounce starts on a primitive), and  \
+               they all start at the camera: one uniform flag, set on the host (wideFar) */     \
+            if (kargs()->camFar && depthLeft + 1 == kargs()->max_depth) {                           \
                 ng = 0u;       /* origin far from the scene: no wide traversal, */                 \
                 oct |= 8u;     /* the query in the reference's order (SHADE's redo) */             \
             }                                                                                     \
@@ -1170,7 +1145,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
                 poolLeft = grab_;                                                                 \
             }                                                                                     \
-            /* wave-uniform: the taken tasks span task groups (tile slot, block) g0 and g0 + 1 */ \
+            /* wave-uniform: the taken tasks span task groups (tile slot, blocks) g0 and g0 + 1 */ \
             const uint32_t base_ = poolBase;                                                      \
             const uint32_t take_ = min((uint32_t)__popcll(m_), poolLeft);                         \
             poolBase += take_;                                                                    \
@@ -1196,25 +1171,22 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     if (c_ < Q_.width && r_ < Q_.nrows) {                                           \
                         needTask = false;                                                         \
                         got = true;                                                               \
-                        taskRays = 0;                                                             \
-                        cr = (uint32_t)c_ | ((uint32_t)r_ << 16);                                 \
-                        frow = (float)globalRowFast(r_, Q_.stripe_h, Q_.stripeShift, Q_.nparts, Q_.part); \
-                        sample = (int)(hi_ ? blkB_ : blkA_) * Q_.block;                            \
-                        nSamples = min(sample + Q_.block, Q_.spp);                                  \
+                        const uint32_t s0_ = (hi_ ? blkB_ : blkA_) * (uint32_t)Q_.block;          \
+                        taskState[lane] = make_uint4((uint32_t)c_ | ((uint32_t)r_ << 16), s0_,     \
+                                                     min(s0_ + (uint32_t)Q_.block, (uint32_t)Q_.spp), 0u); \
                         sum = f3(0.0f, 0.0f, 0.0f);                                               \
                     }                                                                             \
                 }                                                                                 \
             }                                                                                     \
         }                                                                                         \
     } while (0)
-    // Sample mode: the lane's block is complete -> its sum, cost; ask for the next task.
-#define PT_FINISH_TASK()                                                                            \
+    // Sample mode: the lane's block (= its task; ts = the task state) is complete: its sum and ray
+    // count wait in LDS, the next loop iteration adds them to the pixel's accumulator
+    // (PT_FLUSH_BLOCKS, where few registers are live), and the lane asks for its next task.
+#define PT_FINISH_TASK(ts)                                                                          \
     do {                                                                                          \
-        const uint32_t c_ = cr & 0xffffu, r_ = cr >> 16;                                          \
-        /* the block sum and the task's ray count wait in LDS; the next loop iteration adds them \
-           to the pixel's accumulator (PT_FLUSH_BLOCKS, where few registers are live) */          \
-        flushSum[lane] = make_float4(sum.x, sum.y, sum.z, __uint_as_float(taskRays + 1u));      \
-        flushPix[lane] = r_ * (uint32_t)kargs()->width + c_;                                      \
+        flushSum[lane] = make_float4(sum.x, sum.y, sum.z, __uint_as_float((ts).w + 1u));        \
+        flushPix[lane] = ((ts).x >> 16) * (uint32_t)kargs()->width + ((ts).x & 0xffffu);          \
         flushLane = true;                                                                         \
         needTask = true;                                                                          \
     } while (0)
@@ -1224,10 +1196,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     do {                                                                                          \
         if constexpr (SAMPLE) {                                                                   \
             if (__ballot(flushLane) != 0) {                                                       \
-                if (flushLane) {                                                                  \
+                if (flushLane && !PT_AB_NO_ATOMICS) {                                             \
                     const float4 v_ = flushSum[lane];                                             \
                     addBlock(kargs()->pixAcc + 4 * (size_t)flushPix[lane], f3(v_.x, v_.y, v_.z),  \
-                             __float_as_uint(v_.w));                                              \
+                             __float_as_uint(v_.w), kargs()->measureCost != 0);                   \
                 }                                                                                 \
                 flushLane = false;                                                                \
             }                                                                                     \
@@ -1236,11 +1208,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
         const auto& Q_ = *kargs();                                                                \
-        if constexpr (PARK && !SAMPLE) fcol = (float)(cr & 0xffffu);                              \
-        if constexpr (SAMPLE) {                                                                   \
-            fcol = (float)(cr & 0xffffu);                                                         \
-            g = sampleStream(Q_.seed0, Q_.seed1, Q_.sampleBase + (uint32_t)sample,                   \
-                             (uint32_t)frow * (uint32_t)Q_.width + (cr & 0xffffu));                \
+        if constexpr (SAMPLE) {   /* the task's pixel and next sample from LDS */                \
+            const uint4 ts_ = taskState[lane];                                                    \
+            fcol = (float)(ts_.x & 0xffffu);                                                      \
+            const uint32_t grow_ = (uint32_t)globalRowFast((int)(ts_.x >> 16), Q_.stripe_h, Q_.stripeShift, \
+                                                           Q_.nparts, Q_.part);                  \
+            frow = (float)grow_;                                                                  \
+            g = sampleStream(Q_.seed0, Q_.seed1, Q_.sampleBase + ts_.y,                           \
+                             grow_ * (uint32_t)Q_.width + (ts_.x & 0xffffu));                      \
         }                                                                                         \
         const float u_ = (fcol + g.uniform()) * Q_.invW;                                           \
         const float v_ = (frow + g.uniform()) * Q_.invH;                                           \
@@ -1261,16 +1236,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 PT_TAKE_TASKS(got);
                 if (__ballot(got) == 0) break;
                 if (got) {
-                    depthPaths += (uint32_t)(nSamples - sample);
-                    for (; sample < nSamples; sample++) {
+                    uint4 ts = taskState[lane];
+                    depthPaths += ts.z - ts.y;
+                    for (; ts.y < ts.z; ts.y++) {
+                        taskState[lane].y = ts.y;
                         PT_NEW_PATH();
                         sum = add(sum, sky(d, att));
                     }
-                    PT_FINISH_TASK();
+                    PT_FINISH_TASK(ts);
                 }
                 PT_FLUSH_BLOCKS();
             }
             needTask = false;
+            waveReduceAdd(P.counters + 4, depthPaths);   // (paths counted per lane here)
         }
     } else if (valid) {
         if (P.max_depth <= 0) {
@@ -1288,36 +1266,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     sRays += (uint32_t)__popcll(__ballot(started));
     sPaths += (uint32_t)__popcll(__ballot(started)) +
               (!SAMPLE && P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
-#define PT_PARK()                                                                                   \
-    do {                                                                                          \
-        if constexpr (PARK) {                                                                     \
-            uint32_t* pk_ = park + lane;                                                          \
-            pk_[0 * kWave] = g.d; pk_[1 * kWave] = g.v0; pk_[2 * kWave] = g.v1;                   \
-            pk_[3 * kWave] = g.v2; pk_[4 * kWave] = g.v3; pk_[5 * kWave] = g.v4;                  \
-            pk_[6 * kWave] = __float_as_uint(att.x); pk_[7 * kWave] = __float_as_uint(att.y);     \
-            pk_[8 * kWave] = __float_as_uint(att.z); pk_[9 * kWave] = __float_as_uint(sum.x);     \
-            pk_[10 * kWave] = __float_as_uint(sum.y); pk_[11 * kWave] = __float_as_uint(sum.z);   \
-            pk_[12 * kWave] = (uint32_t)depthLeft; pk_[13 * kWave] = (uint32_t)sample;            \
-            pk_[14 * kWave] = (uint32_t)nSamples; pk_[15 * kWave] = cr;                           \
-            pk_[16 * kWave] = __float_as_uint(frow); pk_[17 * kWave] = taskRays;                  \
-        }                                                                                         \
-    } while (0)
-#define PT_UNPARK()                                                                                 \
-    do {                                                                                          \
-        if constexpr (PARK) {                                                                     \
-            const uint32_t* pk_ = park + lane;                                                    \
-            g = Xorwow{pk_[0 * kWave], pk_[1 * kWave], pk_[2 * kWave], pk_[3 * kWave], pk_[4 * kWave], \
-                       pk_[5 * kWave]};                                                           \
-            att = f3(__uint_as_float(pk_[6 * kWave]), __uint_as_float(pk_[7 * kWave]),             \
-                     __uint_as_float(pk_[8 * kWave]));                                            \
-            sum = f3(__uint_as_float(pk_[9 * kWave]), __uint_as_float(pk_[10 * kWave]),            \
-                     __uint_as_float(pk_[11 * kWave]));                                           \
-            depthLeft = (int)pk_[12 * kWave]; sample = (int)pk_[13 * kWave];                      \
-            nSamples = (int)pk_[14 * kWave]; cr = pk_[15 * kWave];                                \
-            frow = __uint_as_float(pk_[16 * kWave]); taskRays = pk_[17 * kWave];                  \
-        }                                                                                         \
-    } while (0)
-    PT_PARK();
 
     for (;;) {
         PT_FLUSH_BLOCKS();
@@ -1384,27 +1332,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     }
                 }
             } else if (wantNode) {
-#if PT_NODE_BUFFER_LOADS
                 // buffer loads: a 32-bit per-lane offset off a wave-uniform resource (no 64-bit
                 // address arithmetic per visit); < 2^26 nodes (pt_scene_create)
                 const uint32_t off = (uint32_t)node * 64u;
                 const float4 a = bload4(nodeRsrc, off), b = bload4(nodeRsrc, off + 16u);
                 const float4 q = bload4(nodeRsrc, off + 32u), r = bload4(nodeRsrc, off + 48u);
-#else
-                const float4* np = S.nodes + 4 * (size_t)node;
-                const float4 a = np[0], b = np[1], q = np[2], r = np[3];
-#endif
                 const uint32_t lref = __float_as_uint(r.x), rref = __float_as_uint(r.y);
-#if PT_PACKED_SLAB
                 SlabHit2 h2 = slabBoth(a, b, q, o, inv, 0.001f, closest);
                 // keep the right child's packed arithmetic next to the left's (not sunk past the
                 // left child's queue append, where the operand pairs are no longer at hand)
                 asm volatile("" : "+v"(h2.r.lo));
                 const SlabHit hl = h2.l, hr = h2.r;
-#else
-                const SlabHit hl = slabLeft(a, b, o, inv, 0.001f, closest);
-                const SlabHit hr = slabRight(b, q, o, inv, 0.001f, closest);
-#endif
                 // append hit leaves in order (left, then right) with their slab entry distances
                 if constexpr (LQ == 2) {
                     // a NODE step needs an empty queue (qn <= LQ - 2): the slots are fixed
@@ -1498,11 +1436,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             // is empty and the lane rejoins NODE steps; measured -4 % vs one leaf per step).
             // The first two queued primitives are loaded together up front (their addresses are
             // known; only the tests depend on `closest`): one memory round trip for two leaves.
-#if PT_LEAF_PREFETCH
             Prim pf0{}, pf1{};
             if (qn > 0) pf0 = loadPrim(S, qref[0] & kPrimMask);
             if (qn > 1) pf1 = loadPrim(S, qref[1] & kPrimMask);
-#endif
 #pragma unroll
             for (int k_ = 0; k_ < LQ; k_++) {
                 const bool act = qn > 0;
@@ -1520,11 +1456,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 // Exact re-test of the leaf box with the current closest: the box passed when it
                 // was queued, with a tmax >= closest, so now it fails iff closest < lo (slabLo).
                 if (!(closest < lo)) {
-#if PT_LEAF_PREFETCH
                     const Prim pr = k_ == 0 ? pf0 : (k_ == 1 ? pf1 : loadPrim(S, k));
-#else
-                    const Prim pr = loadPrim(S, k);
-#endif
                     // (wide: a leaf that waited on the stack has no entry distance, lo = -inf:
                     // exact re-test of its box from the primitive's vertices)
                     {
@@ -1542,8 +1474,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         if (kind == 2) {
             // ------------------------------------------------------------------ SHADE
             if constexpr (WIDE) {
-                // rare: an order-dependent query, repeated in the reference's order (before the
-                // path state comes back from LDS: only the ray is live here).  Ranks index wshade.
+                // rare: an order-dependent query (or a far origin), repeated in the reference's
+                // order.  Ranks index wshade.
                 const bool redo = wantShade && !needTask && (oct & 8u);
                 PT_DIAG_ADD(sRedo, (uint32_t)__popcll(__ballot(redo)));
                 if (redo) {
@@ -1553,7 +1485,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     best = k >= 0 ? (int)S2.rankOf[k] : -1;
                 }
             }
-            PT_UNPARK();
             bool newRay = false, newSample = false;
             PT_DIAG_ADD(itS, 1u);
             if (wantShade && !needTask) {
@@ -1573,12 +1504,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 }
                 if (done) {
                     sum = add(sum, contrib);
-                    ++sample;
-                    if (sample == nSamples) {
-                        active = false;
-                        if constexpr (SAMPLE) PT_FINISH_TASK();
+                    if constexpr (SAMPLE) {
+                        uint4 ts = taskState[lane];
+                        ts.y++;
+                        taskState[lane].y = ts.y;
+                        if (ts.y == ts.z) {
+                            active = false;
+                            PT_FINISH_TASK(ts);
+                        } else {
+                            newSample = true;
+                        }
                     } else {
-                        newSample = true;
+                        ++sample;
+                        if (sample == nSamples) active = false;
+                        else newSample = true;
                     }
                 }
                 newRay = true;   // bounce, next sample (newSample) or finished (reset below)
@@ -1610,7 +1549,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #endif
             sRays += (uint32_t)__popcll(__ballot(newRay));
             sPaths += (uint32_t)__popcll(__ballot(newSample));
-            PT_PARK();
         }
 #ifdef PT_DIAG
         {   // shader-clock cycles per step kind (the step's memory waits included)
@@ -1622,9 +1560,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #endif
     }
     PT_FLUSH_BLOCKS();   // (the loop ends only when no lane has work: a block closed in its last step)
-    PT_UNPARK();
     if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
-        if constexpr (PARK) idx = (cr >> 16) * (uint32_t)P.width + (cr & 0xffffu);
         if (valid) {
             storePixel(P, idx, sum);
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
@@ -1633,7 +1569,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
     if (!SAMPLE && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
     if constexpr (SAMPLE) {   // max_depth <= 0: paths counted per lane
-        if (P.max_depth <= 0) waveReduceAdd(P.counters + 4, depthPaths);
+
     }
     if (P.waveTimes && lane == 0) {
         unsigned xcc;
@@ -1667,8 +1603,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     }
 }
 #undef PT_BEGIN_RAY
-#undef PT_PARK
-#undef PT_UNPARK
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK
@@ -2315,6 +2249,7 @@ struct pt_film {
     DevBuf tileCost, tileOrder;   // measured per-tile cost of the last launch; LPT launch order
     DevBuf tileKeys, tileKeys2, tileIds, sortTemp;   // the order's radix sort on the device
     bool haveOrder = false;
+    int framesSinceCost = 0;      // sample mode: frames rendered since the tile costs were last measured
     DevBuf pixAcc, taskCounter;   // sample mode: per-pixel {x, y, z, rays} accumulators; task counter
     DevBuf stackSpill;            // sample mode on deep trees: traversal stack entries beyond LDS
     DevBuf sums;                  // compat mode: raw per-pixel sample sums of the frame (resolve input)
@@ -3126,6 +3061,12 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.nwaves = 0;
     P.seed0 = (uint32_t)f->seed;
     P.seed1 = (uint32_t)(f->seed >> 32);
+    P.measureCost = 0;
+    {   // wideFar (pt_device.hip) for the camera: its rays then take the reference-order path
+        const float m = std::fmax(std::fmax(std::fabs(cam->origin[0] - s->sceneCE[0]), std::fabs(cam->origin[1] - s->sceneCE[1])),
+                                  std::fabs(cam->origin[2] - s->sceneCE[2]));
+        P.camFar = !(m <= 8.0f * s->sceneCE[3]) ? 1 : 0;
+    }
     // Defaults swept on C3 (tools/ab_env.py): sample mode is throughput-bound and prefers full
     // LEAF / SHADE steps.  Compat mode is bound by its slowest pixels' sequential chains: 20 / 12
     // together with nodeMin 8 (C3 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 -> 1,180 against 8 / 12).
@@ -3176,7 +3117,12 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
-        HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));   // rays per tile, over its tasks
+        // Tile costs (rays of the tile's most expensive pixel) are measured on the first frame and
+        // then on one frame in eight: the order only steers the launch's tail, and counting costs
+        // one more atomic per task.
+        P.measureCost = (lpt && (!f->haveOrder || f->framesSinceCost >= 7)) ? 1 : 0;
+        f->framesSinceCost = P.measureCost ? 0 : f->framesSinceCost + 1;
+        if (P.measureCost) HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));
     }
     // Deep trees: stack entries beyond kLdsStack live in memory, per wave slot (persistent wave or
     // compat tile) and lane
@@ -3223,7 +3169,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         resolveKernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(f->sums.as<float>(), sample ? P.pixAcc : nullptr,
                                                                      accumulate ? f->accum.as<float>() : nullptr,
                                                                      inv, fmt, dst, np,
-                                                                     sample ? f->tileCost.as<unsigned>() : nullptr,
+                                                                     P.measureCost ? f->tileCost.as<unsigned>() : nullptr,
                                                                      f->width, P.tiles_x, envInt("PT_TILE_KEY_MAX", 1));
         HIP_TRY(hipGetLastError());
     }
@@ -3234,7 +3180,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(f->ev2, st));
     f->rendered = true;
-    if (lpt && P.ntiles > 0) {   // next launch: longest tiles first (a stable radix sort, on the device)
+    if (lpt && P.ntiles > 0 && (!sample || P.measureCost)) {   // next launches: longest tiles first (a stable radix sort, on the device)
         const int nt = (int)ntl;
         if ((rc = devReserve(f->tileKeys, ntl * 4)) || (rc = devReserve(f->tileKeys2, ntl * 4)) ||
             (rc = devReserve(f->tileIds, ntl * 4)))
