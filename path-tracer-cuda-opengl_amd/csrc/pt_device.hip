@@ -54,9 +54,6 @@ constexpr int kWave = 64;
 #ifndef PT_AB_NO_ATOMICS
 #define PT_AB_NO_ATOMICS 0
 #endif
-#ifndef PT_AB_NO_FAR
-#define PT_AB_NO_FAR 0
-#endif
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kPrimMask = 0x3fffffffu;
@@ -771,6 +768,9 @@ __device__ __forceinline__ float fixedToFloat(unsigned long long a) { return (fl
 // count; no-return atomics (device scope: 4 of them per task cost 5 % of a C3 frame, so the ray
 // counts are taken on one frame in eight).
 __device__ __forceinline__ void addBlock(unsigned long long* acc, float3 sum, uint32_t rays, bool cost) {
+#if PT_AB_NO_ATOMICS
+    return;
+#endif
     __hip_atomic_fetch_add(acc + 0, blockFixed(sum.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(acc + 1, blockFixed(sum.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(acc + 2, blockFixed(sum.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1016,10 +1016,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     constexpr int SPECN = WIDE ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
     __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
-    // sample mode: each lane's last finished block {sum, rays} and its pixel, until flushed
-    __shared__ float4 flushSum[SAMPLE ? kWave : 1];
-    __shared__ uint32_t flushPix[SAMPLE ? kWave : 1];
-    bool flushLane = false;
     // sample mode: the lane's task {pixel col | local row << 16, next sample, end sample, rays}.
     // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
     // in four VGPRs carried through every step.
@@ -1084,6 +1080,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     bool needTask = SAMPLE;
     uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode: the wave's reserved tasks (uniform)
 
+
     // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
     // captured variables address-taken and they end up in scratch memory.)
 #define PT_BEGIN_RAY()                                                                              \
@@ -1137,10 +1134,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             if (m_ == 0) break;                                                                   \
             if (poolLeft == 0u) { /* refill the wave's pool: one returning atomic per kTaskPool */ \
                 const int leader_ = __ffsll((unsigned long long)m_) - 1;                          \
-                uint32_t b_ = 0;                                                                  \
                 /* always a full pool: = one (tile, block) group, one task per lane; smaller    \
                    grabs near the end measured slower (1/8 share: 150-158 vs 145 ms) */          \
                 const uint32_t grab_ = (uint32_t)kTaskPool;                                       \
+                uint32_t b_ = 0;                                                                  \
                 if (lane == leader_) b_ = atomicAdd(Q_.taskCounter, grab_);                        \
                 poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
                 poolLeft = grab_;                                                                 \
@@ -1181,29 +1178,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }                                                                                         \
     } while (0)
     // Sample mode: the lane's block (= its task; ts = the task state) is complete: its sum and ray
-    // count wait in LDS, the next loop iteration adds them to the pixel's accumulator
-    // (PT_FLUSH_BLOCKS, where few registers are live), and the lane asks for its next task.
+    // count go to the pixel's accumulator (order-free integer atomics on per-pixel addresses: no
+    // contention; right here -- deferring them to a later step of the loop, where fewer registers
+    // are live, measured 2.6 % slower), and the lane asks for its next task.
 #define PT_FINISH_TASK(ts)                                                                          \
     do {                                                                                          \
-        flushSum[lane] = make_float4(sum.x, sum.y, sum.z, __uint_as_float((ts).w + 1u));        \
-        flushPix[lane] = ((ts).x >> 16) * (uint32_t)kargs()->width + ((ts).x & 0xffffu);          \
-        flushLane = true;                                                                         \
+        addBlock(kargs()->pixAcc + 4 * (size_t)(((ts).x >> 16) * (uint32_t)kargs()->width + ((ts).x & 0xffffu)), \
+                 sum, (ts).w + 1u, kargs()->measureCost != 0);                                    \
         needTask = true;                                                                          \
-    } while (0)
-    // Finished blocks -> their pixels' accumulators: order-free integer atomics on per-pixel
-    // addresses (no contention).  At the top of the step loop, a uniform branch.
-#define PT_FLUSH_BLOCKS()                                                                           \
-    do {                                                                                          \
-        if constexpr (SAMPLE) {                                                                   \
-            if (__ballot(flushLane) != 0) {                                                       \
-                if (flushLane && !PT_AB_NO_ATOMICS) {                                             \
-                    const float4 v_ = flushSum[lane];                                             \
-                    addBlock(kargs()->pixAcc + 4 * (size_t)flushPix[lane], f3(v_.x, v_.y, v_.z),  \
-                             __float_as_uint(v_.w), kargs()->measureCost != 0);                   \
-                }                                                                                 \
-                flushLane = false;                                                                \
-            }                                                                                     \
-        }                                                                                         \
     } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
@@ -1245,7 +1227,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     }
                     PT_FINISH_TASK(ts);
                 }
-                PT_FLUSH_BLOCKS();
             }
             needTask = false;
             waveReduceAdd(P.counters + 4, depthPaths);   // (paths counted per lane here)
@@ -1268,7 +1249,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
               (!SAMPLE && P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
 
     for (;;) {
-        PT_FLUSH_BLOCKS();
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
@@ -1559,7 +1539,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }
 #endif
     }
-    PT_FLUSH_BLOCKS();   // (the loop ends only when no lane has work: a block closed in its last step)
     if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
         if (valid) {
             storePixel(P, idx, sum);
@@ -1606,7 +1585,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK
-#undef PT_FLUSH_BLOCKS
 #undef PT_DIAG_ADD
 
 // Frame epilogue (one lane per pixel).  The frame's linear sum S is the raw compat sum
