@@ -237,8 +237,17 @@ def main() -> None:
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
     ref_st = frame(ptamd.KERNEL_SIMPLE)
     ref_buf.copy_(local_buf)
+
+    def check(st):
+        # every frame: this rank's pixels and ray count equal the reference-order frame's
+        if st.rays != ref_st.rays or not torch.equal(local_buf, ref_buf) or (
+                args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
+                                                st.sphere_tests != ref_st.sphere_tests)):
+            raise SystemExit("frame differs from the reference-order frame")
+
+    check(ref_st)   # (also loads torch's comparison kernels before the timed region)
     for _ in range(max(0, args.warmup - 1)):
-        frame()
+        check(frame())
     if args.kernel == "wide":   # the wide tree was built at the first wide render (host binned SAH)
         scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]
     if world > 1:
@@ -250,11 +259,7 @@ def main() -> None:
     spec_visits = 0
     for _ in range(args.steps):
         st = frame()
-        # every timed frame: this rank's pixels and ray count equal the reference-order frame's
-        if st.rays != ref_st.rays or not torch.equal(local_buf, ref_buf) or (
-                args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
-                                                st.sphere_tests != ref_st.sphere_tests)):
-            raise SystemExit("frame differs from the reference-order frame")
+        check(st)
         rays += st.rays
         # algorithmic bytes of the tree the kernel traverses: the wide kernel's own visits; the
         # binary kernel's reference-order visits (its speculative extra visits are not work)

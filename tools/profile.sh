@@ -1,7 +1,9 @@
 #!/bin/bash
 # Bench + rocprofv3 session on the GPU box (run via gpurun).  TAG names the output dir.
 #  1. python bench.py (the driver's default command)          -> gpurun_out/$TAG/bench.json
-#  2. rocprofv3 --kernel-trace --stats of the same command      -> gpurun_out/$TAG/trace/
+#  2. rocprofv3 --kernel-trace --stats of the same frames (without the CPU baseline and the
+#     interactive-mode frames, whose 1-16 spp launches would mix into the render kernel's average)
+#                                                               -> gpurun_out/$TAG/trace/
 #  3. separate --pmc passes (FETCH_SIZE | WRITE_SIZE | TCC hit/miss | SQ | VALU instructions) on one frame
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -10,7 +12,8 @@ TAG=${TAG:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 BENCH_ARGS=${BENCH_ARGS:-}
-PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-compat}
+PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-compat --no-interactive}
+TRACE_ARGS=${TRACE_ARGS:---no-cpu-baseline --no-interactive}
 step() {  # name, limit, command...
     local name=$1 lim=$2; shift 2
     timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1
@@ -20,7 +23,7 @@ step() {  # name, limit, command...
 }
 step bench 600 python bench.py $BENCH_ARGS
 grep '^{' $OUT/bench.log > $OUT/bench.json
-step trace 900 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $BENCH_ARGS
+step trace 900 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $TRACE_ARGS $BENCH_ARGS
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
 step pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $OUT/pmc_tcc -o run --output-format csv -- python3 bench.py $PMC_ARGS $BENCH_ARGS
