@@ -56,7 +56,10 @@ CONFIGS = {
     "c2": ("cornell", "Cornell box (32 tris) 800x800 @256spp depth 8 (C2)"),
     "c5": ("bunny_field", "1,043,312-tri bunny field 1920x1080 @512spp depth 16 (C5)"),
     "c4": ("bunny_cornell", "bunny-in-Cornell (5,000 tris) 1920x1080 @4096spp depth 50 (C4, the 8-GPU config)"),
+    "c5i": ("bunny_field", "bunny field instanced: 5,000 tris stored once, 211 instances (1,043,312 tris placed) "
+                           "1920x1080 @512spp depth 16 (C5, two-level tree)"),
 }
+INSTANCED = {"c5i"}
 CONFIG_SPP = {"c4": 4096}
 STRIPE = 8
 
@@ -193,12 +196,21 @@ def main() -> None:
             dist.init_process_group(backend)
 
     name, workload = CONFIGS[args.config]
-    preset = ptamd.Preset(name)
+    instanced = args.config in INSTANCED
+    if instanced and args.kernel != "wide":
+        raise SystemExit("instanced scenes render with the wide kernel")
+    preset = ptamd.InstancedPreset(name) if instanced else ptamd.Preset(name)
     spp = args.spp or CONFIG_SPP.get(args.config, preset.spp)
     w, h, depth = preset.width, preset.height, preset.max_depth
-    scene = ptamd.Scene(preset.objects, preset.materials, device=local)
-    scene.build_bvh()   # again: the first build in a process also pays one-time module loading
-    scene_build = {"lbvh_device_ms": scene.build_ms}
+    if instanced:
+        scene = ptamd.Scene.instanced(preset.objects, preset.mesh_first, preset.mesh_count, preset.instances,
+                                      preset.materials, device=local)
+        scene.build_bvh()
+        scene_build = {"two_level_tree_host_ms": scene.build_ms, "device_bytes": scene.bvh_info()["device_bytes"]}
+    else:
+        scene = ptamd.Scene(preset.objects, preset.materials, device=local)
+        scene.build_bvh()   # again: the first build in a process also pays one-time module loading
+        scene_build = {"lbvh_device_ms": scene.build_ms}
     film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
     max_rows = ptdist.max_rows(h, STRIPE, world)
     rgba8 = args.output == "rgba8"
@@ -235,7 +247,8 @@ def main() -> None:
     # order exactly: its counters give the frame's ALGORITHMIC bytes (the wavefront kernel may
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
-    ref_st = frame(ptamd.KERNEL_SIMPLE)
+    # (An instanced scene has only the wide kernel: its first frame is the one later frames equal.)
+    ref_st = frame(ptamd.KERNEL_WIDE if instanced else ptamd.KERNEL_SIMPLE)
     ref_buf.copy_(local_buf)
 
     def check(st):
@@ -248,7 +261,7 @@ def main() -> None:
     check(ref_st)   # (also loads torch's comparison kernels before the timed region)
     for _ in range(max(0, args.warmup - 1)):
         check(frame())
-    if args.kernel == "wide":   # the wide tree was built at the first wide render (host binned SAH)
+    if args.kernel == "wide" and not instanced:   # built at the first wide render (host binned SAH)
         scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]
     if world > 1:
         dist.barrier()
@@ -380,7 +393,7 @@ def main() -> None:
             out["compat_mode"] = compat
         if world == 1 and not args.no_interactive:
             out["interactive"] = interactive(scene, preset, dev, stream, local)
-        if world == 1:   # the per-frame rebuild of a dynamic scene: LBVH + wide tree, both on the device
+        if world == 1 and not instanced:   # a dynamic scene's per-frame rebuild: LBVH + wide tree on the device
             dyn = ptamd.Scene(preset.objects, preset.materials, device=local,
                               flags=ptamd.PT_BVH_ORIGIN_BOUNDS | ptamd.PT_BVH_WIDE_DEVICE)
             dyn.build_bvh(ptamd.PT_BVH_ORIGIN_BOUNDS | ptamd.PT_BVH_WIDE_DEVICE)   # a rebuild: buffers reused
@@ -388,7 +401,7 @@ def main() -> None:
             del dyn
         out["scene_build"] = scene_build
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(preset)
+            out["cpu_baseline"] = cpu_baseline(ptamd.Preset(name) if instanced else preset)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

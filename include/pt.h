@@ -78,6 +78,21 @@ typedef struct {
     char name[64];
 } pt_scene_desc;
 
+/* Instancing.  An instance places mesh `mesh` (a range of objects, in object
+ * space) in the world by the affine transform world = m * (object, 1), m row-major 3 x 4. */
+typedef struct { float m[12]; int32_t mesh; int32_t reserved; } pt_instance;
+/* An instanced scene description (pt_preset_instanced): meshes = object ranges
+ * [mesh_first[i], mesh_first[i] + mesh_count[i]) of `objects`. */
+typedef struct {
+    pt_object* objects; int64_t n_objects;
+    int64_t* mesh_first; int64_t* mesh_count; int32_t n_meshes;
+    pt_instance* instances; int64_t n_instances;
+    pt_material* materials; int64_t n_materials;
+    pt_camera camera;
+    int32_t width, height, spp, max_depth;
+    char name[64];
+} pt_instanced_desc;
+
 typedef struct pt_scene pt_scene;   /* device-resident objects, materials, LBVH */
 typedef struct pt_film pt_film;     /* device-resident per-pixel RNG streams for a set of rows */
 
@@ -97,6 +112,12 @@ int pt_camera_move(pt_camera* cam, int dir, float delta_time);
  * cornellbox/<part>.obj and bunny/bunny.obj.  width/height <= 0 keep the preset's frame. */
 int pt_preset_scene(const char* name, const char* models_dir, int width, int height, pt_scene_desc* out);
 void pt_scene_desc_free(pt_scene_desc* desc);
+/* The instanced form of a preset: "bunny_field" (C5: the Cornell box once and the bunny mesh,
+ * scaled x250 in object space, placed 210 times by translations -- the same grid, order and frame
+ * as pt_preset_scene's flattened 1,043,312 triangles), "bunny_cornell" (box + one bunny), "cornell"
+ * (the box alone).  The box is instance 0 with the identity transform. */
+int pt_preset_instanced(const char* name, const char* models_dir, int width, int height, pt_instanced_desc* out);
+void pt_instanced_desc_free(pt_instanced_desc* desc);
 /* OBJ mesh -> triangle objects (objl::Loader::LoadFile, OBJ_Loader.hpp:426-708, flattened to
  * one pt_object per triangle); v' = v * scale + translate.  *out is freed with pt_free. */
 int pt_load_obj(const char* path, float scale, const float translate[3], int32_t mat,
@@ -139,6 +160,20 @@ int pt_scene_build_bvh(pt_scene* scene, int flags);
  * stream) instead of the null stream; returns when the build is complete (the tree depth is read
  * back to pick the traversal kernel). */
 int pt_scene_build_bvh_ex(pt_scene* scene, int flags, void* stream);
+/* An instanced scene (the reference has none: its MeshLoader is a stub,
+ * mesh_loader.h:9-16, and every triangle is its own object with its own cudaMalloc, main.cu:182-190).
+ * Each mesh is stored once, in object space; pt_scene_build_bvh builds a two-level tree: one
+ * bottom-level 8-wide tree per mesh and a top-level tree over the instances' world boxes, all in
+ * one node array.  Rays enter an instance transformed by the inverse of its matrix (the hit's t is
+ * the same parameter in both spaces); normals return by the inverse transpose.  Renders and traces
+ * use the wide kernel only (PT_KERNEL_WIDE or PT_KERNEL_DEFAULT).  Because the ray is transformed,
+ * results equal the flattened scene's within floating-point tolerance (tests/test_gpu_instancing.py
+ * states it), not bit for bit; ties between equal t are decided by (instance, primitive).  Hit
+ * records report obj = the object's index in the flattened order (instances in order, each
+ * contributing its mesh's objects). */
+int pt_scene_create_instanced(int device, const pt_object* objs, int64_t n_objects, const int64_t* mesh_first,
+                              const int64_t* mesh_count, int n_meshes, const pt_instance* instances, int64_t n_instances,
+                              const pt_material* mats, int64_t n_materials, pt_scene** out);
 /* Dynamic scenes (per-frame rebuild): overwrite objects [first, first + n)
  * (host array; same validation as pt_scene_create) and mark the hierarchy stale -- rendering or
  * tracing fails with PT_ERR_STATE until pt_scene_build_bvh runs again.  A rebuild reuses every

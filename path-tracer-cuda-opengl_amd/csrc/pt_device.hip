@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -75,7 +76,15 @@ struct DevScene {
     int nprims;
     int hasSpheres;          // 0: triangles only (the wide kernels' LEAF tests drop the sphere tie rules)
     float cx, cy, cz, ext;   // tight scene box: centre and largest extent (the wide kernels' far-origin test)
+    // instanced scenes (renderKernelWF<.., INST>): per instance {world-to-object rows r0, r1, r2}
+    // {objBase, identity, 0, 0}; a hit's key is instance << gBits | its primitive's shading index
+    const float4* winst;
+    int gBits;
 };
+// Instancing: the stack entry that returns a lane from an instance's bottom-level tree to the world
+// (a child base of 2^24 - 1 never exists); the exponent word of an instance record (pt_wide8.hpp).
+constexpr uint32_t kInstMarker = 0xffffffffu;
+constexpr uint32_t kInstFlag = 0xff000000u;
 
 struct DevCamera {
     float3 pos, ll, hor, ver;
@@ -366,11 +375,12 @@ __device__ __forceinline__ SlabHit refLeafBox(const Prim& q, bool sphere, float3
 // fewer instructions.
 template <bool SPH>
 __device__ __forceinline__ void wideTest(const Prim& q, float3 o, float3 d, float3 inv, float tmin, float& closest,
-                                         int& best, float& bestLo, bool leafBoxes, bool& redo) {
+                                         int& best, float& bestLo, bool leafBoxes, bool& redo, uint32_t keyHi = 0u) {
     const bool sph = SPH && __float_as_uint(q.p2.w) != 0u;
     const float t = primHitAny(q, sph, o, d, tmin);
     if (t >= 0.0f) {
-        const int k = (int)__float_as_uint(q.p0.w);
+        // (instanced scenes: the instance id above the shading index, keyHi = instance << gBits)
+        const int k = (int)(keyHi | __float_as_uint(q.p0.w));
         const bool none = best < 0, bSph = SPH && (best & (int)kSphereBit) != 0;
         const int bk = SPH ? best & (int)kPrimMask : best;
         const bool tie = sph ? (none || !bSph || k > bk) : (!none && !bSph && k < bk);
@@ -575,6 +585,54 @@ __device__ __forceinline__ HitRec makeHitFrom(const float4* shade, int k, float 
 }
 __device__ __forceinline__ HitRec makeHit(const DevScene& S, int k, float t, float3 o, float3 d) {
     return makeHitFrom(S.shade, k, t, o, d);
+}
+
+// Instanced scenes: the world ray (o, d) entering an instance, in its object space (rows r0..r2 of
+// the world-to-object transform; the hit distance t is the same parameter in both spaces).
+__device__ __forceinline__ float3 xformPoint(float4 r0, float4 r1, float4 r2, float3 p) {
+    return f3(((r0.x * p.x + r0.y * p.y) + r0.z * p.z) + r0.w, ((r1.x * p.x + r1.y * p.y) + r1.z * p.z) + r1.w,
+              ((r2.x * p.x + r2.y * p.y) + r2.z * p.z) + r2.w);
+}
+__device__ __forceinline__ float3 xformDir(float4 r0, float4 r1, float4 r2, float3 v) {
+    return f3((r0.x * v.x + r0.y * v.y) + r0.z * v.z, (r1.x * v.x + r1.y * v.y) + r1.z * v.z,
+              (r2.x * v.x + r2.y * v.y) + r2.z * v.z);
+}
+// Hit record of instance key `key` (instance << gBits | shading index) at distance t of the world
+// ray: the object-space shading record, the outward normal returned to the world by the inverse
+// transpose and normalised (cuda_object.h:62-67 / 85-88 in object space, hit_record.h:21-24 in the
+// world); an instance whose linear part is the identity (a translation) keeps the record's normal as
+// is, the flattened scene's arithmetic.
+__device__ __forceinline__ HitRec makeHitInst(const DevScene& S, uint32_t key, float t, float3 o, float3 d, int& obj) {
+    const uint32_t inst = key >> S.gBits, g = key & ((1u << S.gBits) - 1u);
+    const float4* ir = S.winst + 4 * (size_t)inst;
+    const float4 r0 = ir[0], r1 = ir[1], r2 = ir[2], ex = ir[3];
+    const float4* r = S.wshade + 3 * (size_t)g;
+    const float4 s0 = r[0], s1 = r[1], s2 = r[2];
+    const uint32_t tf = __float_as_uint(s2.y);
+    const bool ident = __float_as_uint(ex.y) == 1u, linIdent = __float_as_uint(ex.y) != 0u;
+    HitRec h;
+    h.p = add(o, scale(t, d));
+    float3 outward;
+    if (tf >> 16) {   // sphere: (p - c) / r in object space
+        const float3 po = ident ? h.p : xformPoint(r0, r1, r2, h.p);
+        outward = divs(sub(po, xyz(s0)), s0.w);
+    } else {
+        outward = xyz(s0);
+    }
+    if (!linIdent) {   // n_world = normalize(A^-T n_object): A^-1's columns dotted with n
+        const float3 n = outward;
+        outward = normalize3(f3((r0.x * n.x + r1.x * n.y) + r2.x * n.z, (r0.y * n.x + r1.y * n.y) + r2.y * n.z,
+                                (r0.z * n.x + r1.z * n.y) + r2.z * n.z));
+    }
+    h.front = dot3(d, outward) < 0.0f;
+    h.n = h.front ? outward : neg(outward);
+    h.mat = (int)__float_as_uint(s2.z);
+    obj = (int)(__float_as_uint(ex.x) + __float_as_uint(s2.w));   // the object's index in the flattened order
+    h.obj = obj;
+    h.m0 = s1;
+    h.ir = s2.x;
+    h.type = (int)(tf & 0xffffu);
+    return h;
 }
 
 // ------------------------------------------------------------------------ BSDFs
@@ -1001,10 +1059,16 @@ __device__ __forceinline__ DevScene ldScene(KArgs k) {
     S.iparent = k->S.iparent; S.err = k->S.err; S.nprims = k->S.nprims;
     S.hasSpheres = k->S.hasSpheres;
     S.cx = k->S.cx; S.cy = k->S.cy; S.cz = k->S.cz; S.ext = k->S.ext;
+    S.winst = k->S.winst; S.gBits = k->S.gBits;
     return S;
 }
 
-template <int STACK, bool SAMPLE, bool WIDE>
+// INST (with WIDE): an instanced scene's two-level tree (pt_scene_create_instanced): a NODE step
+// that reaches an instance record moves the lane's ray into the instance's object space and its
+// bottom-level tree, a stack marker brings it back; no speculative traversal (a parked primitive
+// group would belong to another space), no reference-order redo (instanced frames are held to a
+// tolerance, not bit for bit).
+template <int STACK, bool SAMPLE, bool WIDE, bool INST = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
     // Deep trees (binary kernels) keep 32 stack entries per lane in LDS (8 KB per wave: 5 waves
     // per SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
@@ -1013,9 +1077,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
     // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
     // marks it) and comes back when the current group is empty.
-    constexpr int SPECN = WIDE ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
+    constexpr int SPECN = (WIDE && !INST) ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
     __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
+    // instanced scenes: the lane's world ray {o, d} while it is inside an instance
+    __shared__ float wray[INST ? 6 * kWave : 1];
     // sample mode: the lane's task {pixel col | local row << 16, next sample, end sample, rays}.
     // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
     // in four VGPRs carried through every step.
@@ -1103,7 +1169,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             ng = S.nprims > 0 ? (1u << oc_) : 0u;                                                 \
             /* only camera rays can start far from the scene (a bounce starts on a primitive), and  \
                they all start at the camera: one uniform flag, set on the host (wideFar) */     \
-            if (kargs()->camFar && depthLeft + 1 == kargs()->max_depth) {                           \
+            if (!INST && kargs()->camFar && depthLeft + 1 == kargs()->max_depth) {                 \
                 ng = 0u;       /* origin far from the scene: no wide traversal, */                 \
                 oct |= 8u;     /* the query in the reference's order (SHADE's redo) */             \
             }                                                                                     \
@@ -1279,7 +1345,56 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 PT_DIAG_ADD(sSpecN, (unsigned long long)__popcll(__ballot(tg != 0u && ((ng & 0xffu) != 0u || sp > 0))));
                 PT_DIAG_ADD(sIdleN, (unsigned long long)(64 - nN));
             }
-            if constexpr (WIDE) {
+            if constexpr (INST) {
+                if (wantNode) {
+                    // pop to a group with children left; a marker returns the lane to the world
+                    while ((ng & 0xffu) == 0u && sp > 0) {
+                        sp--;
+                        ng = my[sp * kWave];
+                        if (ng == kInstMarker) {
+                            o = f3(wray[0 * kWave + lane], wray[1 * kWave + lane], wray[2 * kWave + lane]);
+                            d = f3(wray[3 * kWave + lane], wray[4 * kWave + lane], wray[5 * kWave + lane]);
+                            inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                            oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                            ng = 0u;
+                        }
+                    }
+                    if (ng & 0xffu) {
+                        const uint32_t bit = (uint32_t)__builtin_ctz(ng & 0xffu);
+                        const uint32_t child = (ng >> 8) + (bit ^ (oct & 7u));
+                        ng &= ~(1u << bit);
+                        if (ng & 0xffu) { my[sp * kWave] = ng; sp++; }
+                        const uint32_t off = mul80(child);
+                        const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+                        const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+                        const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+                        const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+                        const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+                        if (n0.w == kInstFlag) {   // an instance: into its object space and bottom-level tree
+                            wray[0 * kWave + lane] = o.x; wray[1 * kWave + lane] = o.y; wray[2 * kWave + lane] = o.z;
+                            wray[3 * kWave + lane] = d.x; wray[4 * kWave + lane] = d.y; wray[5 * kWave + lane] = d.z;
+                            if (n0.x == 0u) {   // (an identity instance keeps the world ray)
+                                const float4 r0 = __builtin_bit_cast(float4, n2), r1 = __builtin_bit_cast(float4, n3),
+                                             r2 = __builtin_bit_cast(float4, n4);
+                                o = xformPoint(r0, r1, r2, o);
+                                d = xformDir(r0, r1, r2, d);
+                                inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                            }
+                            const uint32_t oc = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                            my[sp * kWave] = kInstMarker;   // (depth: host check, wideStackFor)
+                            sp++;
+                            ng = (n1.x << 8) | (1u << oc);
+                            oct = oc | (n1.y << 8);   // bits 8+: the instance the lane is in
+                            tg = 0u;
+                        } else {
+                            const uint32_t hits = wideHits(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
+                            ng = (n1.x << 8) | (hits >> 24);
+                            tgBase = n1.y;
+                            tg = hits & 0xffffffu;
+                        }
+                    }
+                }
+            } else if constexpr (WIDE) {
                 if (wantNode) {
                     if (SPEC && tg != 0u) {   // park the waiting primitive group, keep traversing
                         const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
@@ -1393,15 +1508,18 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 const float4* w1 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(k1));
                 const Prim q0{w0[0], w0[1], w0[2]}, q1{w1[0], w1[1], w1[2]};
                 bool redo = false;
+                // (instanced: no reference leaf-box rule; the hit key carries the instance)
+                const bool lb = !INST && S.nprims > 1;
+                const uint32_t kh = INST ? (oct >> 8) << kargs()->S.gBits : 0u;
                 if (kargs()->S.hasSpheres) {   // (uniform: read where needed)
-                    if (h0) wideTest<true>(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
-                    if (h1) wideTest<true>(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                    if (h0) wideTest<true>(q0, o, d, inv, 0.001f, closest, best, bestLo, lb, redo, kh);
+                    if (h1) wideTest<true>(q1, o, d, inv, 0.001f, closest, best, bestLo, lb, redo, kh);
                     const bool s0 = __float_as_uint(q0.p2.w) != 0u, s1 = __float_as_uint(q1.p2.w) != 0u;
                     sTris += (uint32_t)__popcll(__ballot(h0 && !s0)) + (uint32_t)__popcll(__ballot(h1 && !s1));
                     sSph += (uint32_t)__popcll(__ballot(h0 && s0)) + (uint32_t)__popcll(__ballot(h1 && s1));
                 } else {
-                    if (h0) wideTest<false>(q0, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
-                    if (h1) wideTest<false>(q1, o, d, inv, 0.001f, closest, best, bestLo, S.nprims > 1, redo);
+                    if (h0) wideTest<false>(q0, o, d, inv, 0.001f, closest, best, bestLo, lb, redo, kh);
+                    if (h1) wideTest<false>(q1, o, d, inv, 0.001f, closest, best, bestLo, lb, redo, kh);
                     sTris += (uint32_t)__popcll(__ballot(h0)) + (uint32_t)__popcll(__ballot(h1));
                 }
                 if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
@@ -1474,7 +1592,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     contrib = sky(d, att);
                     done = true;
                 } else {
-                    HitRec h = WIDE ? makeHitFrom(kargs()->S.wshade, best & (int)kPrimMask, closest, o, d) : makeHit(S, best, closest, o, d);
+                    int objI_;
+                    HitRec h = INST ? makeHitInst(ldScene(kargs()), (uint32_t)best & kPrimMask, closest, o, d, objI_)
+                                    : (WIDE ? makeHitFrom(kargs()->S.wshade, best & (int)kPrimMask, closest, o, d)
+                                            : makeHit(S, best, closest, o, d));
                     if (!scatterInto(h, d, att, g)) {
                         done = true;
                     } else {
@@ -1697,8 +1818,9 @@ __global__ __launch_bounds__(kWave) void traceKernel(DevScene S, const pt_ray* r
 }
 
 // pt_trace_closest on the wide tree (PT_KERNEL_WIDE): the same traversal as renderKernelWF's
-// WIDE steps, one lane per ray, the same hit records as traceKernel.
-template <int STACK>
+// WIDE steps, one lane per ray, the same hit records as traceKernel.  INST: an instanced scene's
+// two-level tree (renderKernelWF<.., INST>).
+template <int STACK, bool INST>
 __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ray* rays, int64_t n, float tmin,
                                                          float tmax, pt_hit* hits, unsigned long long* counters) {
     __shared__ uint32_t stk[STACK * kWave];
@@ -1710,10 +1832,12 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
     const int64_t i = base + lane;
     if (i < n) {
         const pt_ray r = rays[i];
-        const float3 o = f3(r.o[0], r.o[1], r.o[2]), d = f3(r.d[0], r.d[1], r.d[2]);
-        const float3 inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
-        const uint32_t oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
-        const bool far = wideFar(S, o);   // (then: the query in the reference's order only)
+        const float3 wo = f3(r.o[0], r.o[1], r.o[2]), wd = f3(r.d[0], r.d[1], r.d[2]);
+        const float3 winv = f3(rcpRN(wd.x), rcpRN(wd.y), rcpRN(wd.z));
+        const uint32_t woct = (winv.x < 0.0f ? 1u : 0u) | (winv.y < 0.0f ? 2u : 0u) | (winv.z < 0.0f ? 4u : 0u);
+        float3 o = wo, d = wd, inv = winv;   // (inside an instance: its object space)
+        uint32_t oct = woct, inst = 0u;
+        const bool far = !INST && wideFar(S, o);   // (then: the query in the reference's order only)
         float closest = tmax;
         int best = -1, sp = 0;
         bool redo = far;
@@ -1728,10 +1852,19 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 const Prim q{w[0], w[1], w[2]};
                 if (__float_as_uint(q.p2.w) != 0u) c.spheres++;
                 else c.tris++;
-                if (S.hasSpheres) wideTest<true>(q, o, d, inv, tmin, closest, best, bestLo, S.nprims > 1, redo);
-                else wideTest<false>(q, o, d, inv, tmin, closest, best, bestLo, S.nprims > 1, redo);
+                const bool lb = !INST && S.nprims > 1;
+                const uint32_t kh = INST ? inst << S.gBits : 0u;
+                if (S.hasSpheres) wideTest<true>(q, o, d, inv, tmin, closest, best, bestLo, lb, redo, kh);
+                else wideTest<false>(q, o, d, inv, tmin, closest, best, bestLo, lb, redo, kh);
             }
-            if ((ng & 0xffu) == 0u) {
+            if constexpr (INST) {   // pop; a marker returns to the world ray
+                while ((ng & 0xffu) == 0u && sp > 0) {
+                    sp--;
+                    ng = my[sp * kWave];
+                    if (ng == kInstMarker) { o = wo; d = wd; inv = winv; oct = woct; ng = 0u; }
+                }
+                if ((ng & 0xffu) == 0u) break;
+            } else if ((ng & 0xffu) == 0u) {
                 if (sp == 0) break;
                 sp--;
                 ng = my[sp * kWave];
@@ -1751,6 +1884,23 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
             const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
             const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
             const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+            if (INST && n0.w == kInstFlag) {   // an instance: into its object space and bottom-level tree
+                if (n0.x == 0u) {
+                    const float4 r0 = __builtin_bit_cast(float4, n2), r1 = __builtin_bit_cast(float4, n3),
+                                 r2 = __builtin_bit_cast(float4, n4);
+                    o = xformPoint(r0, r1, r2, wo);
+                    d = xformDir(r0, r1, r2, wd);
+                    inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                    oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                }
+                if (sp >= STACK) { atomicOr(S.err, 2u); break; }
+                my[sp * kWave] = kInstMarker;
+                sp++;
+                ng = (n1.x << 8) | (1u << oct);
+                inst = n1.y;
+                tg = 0u;
+                continue;
+            }
             const uint32_t h = wideHits(n0, n1, n2, n3, n4, o, inv, oct, tmin, closest);
             ng = (n1.x << 8) | (h >> 24);
             tgBase = n1.y;
@@ -1765,7 +1915,9 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
         hr.obj = -1;
         hr.mat = -1;
         if (best >= 0) {
-            HitRec x = makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d);
+            int obj = 0;
+            HitRec x = INST ? makeHitInst(S, (uint32_t)best & kPrimMask, closest, wo, wd, obj)
+                            : makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d);
             hr.hit = 1;
             hr.obj = x.obj;
             hr.mat = x.mat;
@@ -2214,6 +2366,12 @@ struct pt_scene {
     size_t deviceBytes = 0;
     double buildMs = 0.0;                   // last pt_scene_build_bvh, device time (HIP events)
     float sceneCE[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // tight scene box: centre, largest extent (DevScene)
+    // instanced scenes (pt_scene_create_instanced): meshes = object ranges of `objs`, instances
+    bool instanced = false;
+    std::vector<int64_t> meshFirst, meshCount;
+    std::vector<pt_instance> inst;
+    DevBuf winst;                           // per instance: world-to-object rows, {objBase, identity}
+    int gBits = 0;                          // hit key = instance << gBits | shading index
 };
 
 struct pt_film {
@@ -2306,6 +2464,216 @@ int buildWideDevice(pt_scene* s, hipStream_t st) {
     return PT_OK;
 }
 
+// Instanced scenes: the two-level tree, built on the host -- one 8-wide tree per mesh (binned SAH
+// over the mesh's objects in object space), a top-level 8-wide tree over the instances' world boxes
+// with one instance per leaf, whose leaves become instance records (pt_wide8.hpp), all in one node
+// array: the top level from slot 0, then the meshes' trees.  Shading records in object space, one
+// per mesh primitive (its shading index g); the hit key instance << gBits | g.
+int wideStackFor(int depth);
+struct InstRecCtx {
+    const std::vector<std::array<float, 12>>* minv;
+    const std::vector<uint8_t>* ident;
+    const std::vector<pt_instance>* inst;
+};
+uint32_t instanceOfRecord(const uint32_t* rec) { return rec[7]; }
+void writeInstanceRecord(uint32_t id, uint32_t* dst, void* ctx) {
+    const InstRecCtx& c = *static_cast<const InstRecCtx*>(ctx);
+    std::memset(dst, 0, pt::kW8NodeDwords * 4);
+    dst[0] = (*c.ident)[id] ? 1u : 0u;
+    dst[3] = pt::kW8InstanceFlag;
+    dst[4] = (uint32_t)(*c.inst)[id].mesh;   // (the mesh's root slot once the layout is known)
+    dst[5] = id;
+    std::memcpy(dst + 8, (*c.minv)[id].data(), 48);
+}
+
+int buildInstanced(pt_scene* s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int nm = (int)s->meshFirst.size();
+    const int64_t ni = (int64_t)s->inst.size();
+    std::vector<pt::Wide8> blas((size_t)nm);
+    std::vector<uint32_t> shade;   // 12 dwords per mesh primitive
+    std::vector<int64_t> meshG0((size_t)nm, 0);
+    int64_t gTotal = 0;
+    int maxDepthB = 0;
+    std::string err;
+    for (int m = 0; m < nm; m++) {
+        const int64_t n = s->meshCount[(size_t)m], first = s->meshFirst[(size_t)m];
+        meshG0[(size_t)m] = gTotal;
+        std::vector<uint32_t> prims((size_t)n * pt::kW8PrimDwords, 0u), rank((size_t)n);
+        std::vector<float> boxes((size_t)n * 6);
+        shade.resize((size_t)(gTotal + n) * 12, 0u);
+        std::vector<float4> mats((size_t)std::max<int64_t>(1, 2 * s->nmat));
+        HIP_TRY(hipMemcpy(mats.data(), s->mats.p, mats.size() * sizeof(float4), hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < n; k++) {
+            const pt_object& o = s->objs[(size_t)(first + k)];
+            uint32_t* r = &prims[(size_t)k * 12];
+            float* f = reinterpret_cast<float*>(r);
+            float* b = &boxes[(size_t)k * 6];
+            uint32_t* sh = &shade[(size_t)(gTotal + k) * 12];
+            float* shf = reinterpret_cast<float*>(sh);
+            r[3] = (uint32_t)o.mat;
+            r[7] = (uint32_t)k;   // the object within its mesh
+            if (o.type == PT_SPHERE) {
+                f[0] = o.v[0]; f[1] = o.v[1]; f[2] = o.v[2]; f[4] = o.v[3]; r[11] = 1u;
+                const float rr = std::fabs(o.v[3]);
+                for (int a = 0; a < 3; a++) { b[a] = o.v[a] - rr; b[3 + a] = o.v[a] + rr; }
+                shf[0] = o.v[0]; shf[1] = o.v[1]; shf[2] = o.v[2]; shf[3] = o.v[3];
+            } else {
+                for (int v = 0; v < 3; v++)
+                    for (int a = 0; a < 3; a++) f[4 * v + a] = o.v[3 * v + a];
+                for (int a = 0; a < 3; a++) {
+                    b[a] = std::fmin(std::fmin(o.v[a], o.v[3 + a]), o.v[6 + a]);
+                    b[3 + a] = std::fmax(std::fmax(o.v[a], o.v[3 + a]), o.v[6 + a]);
+                }
+                // triangle.h:17-19 normalize(cross(v1 - v0, v2 - v0)), the device's operation order
+                const float e1[3] = {o.v[3] - o.v[0], o.v[4] - o.v[1], o.v[5] - o.v[2]};
+                const float e2[3] = {o.v[6] - o.v[0], o.v[7] - o.v[1], o.v[8] - o.v[2]};
+                const float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+                const float l = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+                if (l != 0.0f) {
+                    const float il = 1.0f / l;
+                    for (int a = 0; a < 3; a++) shf[a] = il * c[a];
+                }
+            }
+            const float4 m0 = mats[(size_t)(2 * o.mat)], m1 = mats[(size_t)(2 * o.mat + 1)];
+            shf[4] = m0.x; shf[5] = m0.y; shf[6] = m0.z; shf[7] = m0.w;
+            uint32_t tp;
+            std::memcpy(&tp, &m1.y, 4);
+            shf[8] = m1.x;
+            sh[9] = tp | (o.type == PT_SPHERE ? 0x10000u : 0u);
+            sh[10] = (uint32_t)o.mat;
+            sh[11] = (uint32_t)k;
+            rank[(size_t)k] = (uint32_t)(gTotal + k);
+        }
+        if (n > 0 && !pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, blas[(size_t)m], err))
+            return fail(PT_ERR_STATE, err);
+        maxDepthB = std::max(maxDepthB, blas[(size_t)m].depth);
+        gTotal += n;
+    }
+    int gBits = 1;
+    while (((int64_t)1 << gBits) < gTotal) gBits++;
+    if (gBits > 28 || ni > ((int64_t)1 << (30 - gBits)))
+        return fail(PT_ERR_INVALID, "instanced scene: too many instances for the hit key (instance << " +
+                                        std::to_string(gBits) + " | primitive)");
+    // instances: world-to-object transforms, world boxes (every mesh vertex transformed, in double)
+    std::vector<std::array<float, 12>> minv((size_t)ni);
+    std::vector<uint8_t> ident((size_t)ni, 0);
+    std::vector<uint32_t> iprims;
+    std::vector<float> iboxes;
+    std::vector<uint32_t> used;
+    std::vector<float> winst((size_t)std::max<int64_t>(1, ni) * 16, 0.0f);
+    uint32_t objBase = 0;
+    for (int64_t i = 0; i < ni; i++) {
+        const pt_instance& I = s->inst[(size_t)i];
+        const double a[3][3] = {{I.m[0], I.m[1], I.m[2]}, {I.m[4], I.m[5], I.m[6]}, {I.m[8], I.m[9], I.m[10]}};
+        const double t[3] = {I.m[3], I.m[7], I.m[11]};
+        const double det = a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+                           a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+        if (!(std::fabs(det) > 1e-30) || !std::isfinite(det))
+            return fail(PT_ERR_INVALID, "instanced scene: instance " + std::to_string(i) + " has a singular transform");
+        double inv[3][3];
+        inv[0][0] = (a[1][1] * a[2][2] - a[1][2] * a[2][1]) / det;
+        inv[0][1] = (a[0][2] * a[2][1] - a[0][1] * a[2][2]) / det;
+        inv[0][2] = (a[0][1] * a[1][2] - a[0][2] * a[1][1]) / det;
+        inv[1][0] = (a[1][2] * a[2][0] - a[1][0] * a[2][2]) / det;
+        inv[1][1] = (a[0][0] * a[2][2] - a[0][2] * a[2][0]) / det;
+        inv[1][2] = (a[0][2] * a[1][0] - a[0][0] * a[1][2]) / det;
+        inv[2][0] = (a[1][0] * a[2][1] - a[1][1] * a[2][0]) / det;
+        inv[2][1] = (a[0][1] * a[2][0] - a[0][0] * a[2][1]) / det;
+        inv[2][2] = (a[0][0] * a[1][1] - a[0][1] * a[1][0]) / det;
+        bool id = true, lin = true;
+        for (int r = 0; r < 3; r++) {
+            const double it = -(inv[r][0] * t[0] + inv[r][1] * t[1] + inv[r][2] * t[2]);
+            for (int c = 0; c < 3; c++) {
+                minv[(size_t)i][(size_t)(4 * r + c)] = (float)inv[r][c];
+                lin = lin && a[r][c] == (r == c ? 1.0 : 0.0);
+            }
+            minv[(size_t)i][(size_t)(4 * r + 3)] = (float)it;
+            id = id && t[r] == 0.0;
+        }
+        id = id && lin;
+        ident[(size_t)i] = id ? 1 : 0;
+        for (int k = 0; k < 12; k++) winst[(size_t)i * 16 + (size_t)k] = minv[(size_t)i][(size_t)k];
+        uint32_t ob = objBase, idf = id ? 1u : lin ? 2u : 0u;   // identity | translation only
+        std::memcpy(&winst[(size_t)i * 16 + 12], &ob, 4);
+        std::memcpy(&winst[(size_t)i * 16 + 13], &idf, 4);
+        objBase += (uint32_t)s->meshCount[(size_t)I.mesh];
+        // world box of the instance
+        const int64_t first = s->meshFirst[(size_t)I.mesh], n = s->meshCount[(size_t)I.mesh];
+        if (n == 0) continue;
+        double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        auto grow = [&](double x, double y, double z) {
+            const double p[3] = {x, y, z};
+            for (int r = 0; r < 3; r++) {
+                const double w = a[r][0] * p[0] + a[r][1] * p[1] + a[r][2] * p[2] + t[r];
+                mn[r] = std::min(mn[r], w);
+                mx[r] = std::max(mx[r], w);
+            }
+        };
+        for (int64_t k = 0; k < n; k++) {
+            const pt_object& o = s->objs[(size_t)(first + k)];
+            if (o.type == PT_SPHERE) {
+                const double rr = std::fabs((double)o.v[3]);
+                for (int c = 0; c < 8; c++)
+                    grow(o.v[0] + ((c & 1) ? rr : -rr), o.v[1] + ((c & 2) ? rr : -rr), o.v[2] + ((c & 4) ? rr : -rr));
+            } else {
+                for (int v = 0; v < 3; v++) grow(o.v[3 * v], o.v[3 * v + 1], o.v[3 * v + 2]);
+            }
+        }
+        iprims.resize(iprims.size() + pt::kW8PrimDwords, 0u);
+        iprims[iprims.size() - pt::kW8PrimDwords + 7] = (uint32_t)i;
+        for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)mn[r], -INFINITY));
+        for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)mx[r], INFINITY));
+        used.push_back((uint32_t)i);
+    }
+    if (used.empty()) return fail(PT_ERR_STATE, "instanced scene: no instance of a non-empty mesh");
+    pt::Wide8 top;
+    if (!pt::buildWide8Leaf(iprims.data(), iboxes.data(), nullptr, (int64_t)used.size(), 1, top, err))
+        return fail(PT_ERR_STATE, err);
+    InstRecCtx ctx{&minv, &ident, &s->inst};
+    if (!pt::instanceLeaves(top, instanceOfRecord, writeInstanceRecord, &ctx, err)) return fail(PT_ERR_STATE, err);
+    // layout: the top level from slot 0, then each mesh's tree (child and primitive bases relocated)
+    const uint32_t topSlots = (uint32_t)(top.nodes.size() / pt::kW8NodeDwords);
+    std::vector<uint32_t> meshRoot((size_t)nm, 0u);
+    uint32_t nodeBase = topSlots, primBase = 0;
+    for (int m = 0; m < nm; m++) {
+        meshRoot[(size_t)m] = nodeBase;
+        pt::relocateWide8(blas[(size_t)m], nodeBase, primBase);
+        nodeBase += (uint32_t)(blas[(size_t)m].nodes.size() / pt::kW8NodeDwords);
+        primBase += (uint32_t)(blas[(size_t)m].prims.size() / pt::kW8PrimDwords);
+    }
+    if ((int64_t)nodeBase >= ((int64_t)1 << 24)) return fail(PT_ERR_STATE, "instanced BVH: more than 2^24 node slots");
+    for (size_t k = 0; k < top.nodes.size(); k += pt::kW8NodeDwords)
+        if (top.nodes[k + 3] == pt::kW8InstanceFlag) top.nodes[k + 4] = meshRoot[top.nodes[k + 4]];
+    std::vector<uint32_t> nodes = top.nodes, prims;
+    for (int m = 0; m < nm; m++) {
+        nodes.insert(nodes.end(), blas[(size_t)m].nodes.begin(), blas[(size_t)m].nodes.end());
+        prims.insert(prims.end(), blas[(size_t)m].prims.begin(), blas[(size_t)m].prims.end());
+    }
+    if (prims.empty()) prims.assign(pt::kW8PrimDwords, 0u);
+    if (shade.empty()) shade.assign(12, 0u);
+    int rc;
+    if ((rc = devReserve(s->wide, nodes.size() * 4)) || (rc = devReserve(s->wprims, prims.size() * 4)) ||
+        (rc = devReserve(s->wshade, shade.size() * 4)) || (rc = devReserve(s->winst, winst.size() * 4)))
+        return rc;
+    HIP_TRY(hipMemcpy(s->wide.p, nodes.data(), nodes.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->wprims.p, prims.data(), prims.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->wshade.p, shade.data(), shade.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->winst.p, winst.data(), winst.size() * 4, hipMemcpyHostToDevice));
+    s->gBits = gBits;
+    s->wideDepth = top.depth + 1 + maxDepthB + 1;   // stack: top levels, the marker, the mesh's levels
+    s->wideNodes = (int64_t)(nodes.size() / pt::kW8NodeDwords);
+    s->wideSource = 3;
+    s->wideReady = true;
+    s->deviceBytes = nodes.size() * 4 + prims.size() * 4 + shade.size() * 4 + winst.size() * 4 + (size_t)s->nmat * 32;
+    s->wideBuildMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    s->buildMs = s->wideBuildMs;
+    s->depth = 0;
+    if (wideStackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "instanced BVH too deep");
+    s->built = true;
+    return PT_OK;
+}
+
 // Traversal stack entries of the wide kernels (one dword per entry): >= the tree depth.
 int wideStackFor(int depth) {
     for (int st : {8, 16, 24})
@@ -2324,6 +2692,11 @@ int setDevice(int dev) {
 
 template <int S>
 void launchRenderWide(const RenderParams& P, hipStream_t st) {
+    if (P.S.winst) {   // an instanced scene's two-level tree
+        if (P.pixAcc) renderKernelWF<S, true, true, true><<<P.nwaves, kWave, 0, st>>>(P);
+        else renderKernelWF<S, false, true, true><<<P.ntiles, kWave, 0, st>>>(P);
+        return;
+    }
     if (P.pixAcc) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
     else renderKernelWF<S, false, true><<<P.ntiles, kWave, 0, st>>>(P);
 }
@@ -2336,13 +2709,21 @@ void launchRender(const RenderParams& P, hipStream_t st) {
     else if (P.pixAcc) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
-template <int S, bool WIDE>
+template <int S, bool WIDE, bool INST = false>
 int wavesPerCU(int& n) {
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&renderKernelWF<S, true, WIDE>),
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&renderKernelWF<S, true, WIDE, INST>),
                                                          kWave, 0));
     return PT_OK;
 }
-int persistentWavesPerCU(int stack, int kernel, int& n) {
+int persistentWavesPerCU(int stack, int kernel, int& n, bool inst = false) {
+    if (kernel == PT_KERNEL_WIDE && inst) {
+        switch (stack) {
+            case 8: return wavesPerCU<8, true, true>(n);
+            case 16: return wavesPerCU<16, true, true>(n);
+            case 24: return wavesPerCU<24, true, true>(n);
+            default: return fail(PT_ERR_STATE, "unsupported instanced BVH depth");
+        }
+    }
     if (kernel == PT_KERNEL_WIDE) {
         switch (stack) {
             case 8: return wavesPerCU<8, true>(n);
@@ -2395,11 +2776,21 @@ int dispatchTrace(int stack, bool wide, const DevScene& S, const pt_ray* r, int6
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const unsigned blocks = (unsigned)std::min<int64_t>((n + kWave - 1) / kWave, (int64_t)cus * 32);
+    if (wide && S.winst) {
+        switch (stack) {
+            case 8: traceKernelWide<8, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 16: traceKernelWide<16, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 24: traceKernelWide<24, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            default: return fail(PT_ERR_STATE, "unsupported instanced BVH depth");
+        }
+        HIP_TRY(hipGetLastError());
+        return PT_OK;
+    }
     if (wide) {
         switch (stack) {
-            case 8: traceKernelWide<8><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
-            case 16: traceKernelWide<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
-            case 24: traceKernelWide<24><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 8: traceKernelWide<8, false><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 16: traceKernelWide<16, false><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+            case 24: traceKernelWide<24, false><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
             default: return fail(PT_ERR_STATE, "unsupported wide BVH depth");
         }
         HIP_TRY(hipGetLastError());
@@ -2447,6 +2838,8 @@ DevScene devScene(const pt_scene* s) {
     S.nprims = (int)s->nobj;
     S.hasSpheres = s->hasSpheres ? 1 : 0;
     S.cx = s->sceneCE[0]; S.cy = s->sceneCE[1]; S.cz = s->sceneCE[2]; S.ext = s->sceneCE[3];
+    S.winst = s->instanced ? s->winst.as<float4>() : nullptr;
+    S.gBits = s->gBits;
     return S;
 }
 
@@ -2549,9 +2942,33 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n, const pt_mater
     return PT_OK;
 }
 
+int pt_scene_create_instanced(int device, const pt_object* objs, int64_t n, const int64_t* mesh_first,
+                              const int64_t* mesh_count, int n_meshes, const pt_instance* inst, int64_t n_inst,
+                              const pt_material* mats, int64_t nmat, pt_scene** out) {
+    if (!out || n < 0 || n_meshes < 0 || n_inst <= 0 || (n > 0 && !objs) || (n_meshes > 0 && (!mesh_first || !mesh_count)) ||
+        !inst || (nmat > 0 && !mats))
+        return fail(PT_ERR_INVALID, "pt_scene_create_instanced: bad argument");
+    for (int m = 0; m < n_meshes; m++)
+        if (mesh_first[m] < 0 || mesh_count[m] < 0 || mesh_first[m] + mesh_count[m] > n)
+            return fail(PT_ERR_INVALID, "pt_scene_create_instanced: mesh range out of bounds");
+    for (int64_t i = 0; i < n_inst; i++)
+        if (inst[i].mesh < 0 || inst[i].mesh >= n_meshes)
+            return fail(PT_ERR_INVALID, "pt_scene_create_instanced: instance of an unknown mesh");
+    pt_scene* s = nullptr;
+    int rc = pt_scene_create(device, objs, n, mats, nmat, &s);
+    if (rc) return rc;
+    s->instanced = true;
+    s->meshFirst.assign(mesh_first, mesh_first + n_meshes);
+    s->meshCount.assign(mesh_count, mesh_count + n_meshes);
+    s->inst.assign(inst, inst + n_inst);
+    *out = s;
+    return PT_OK;
+}
+
 int pt_scene_update_objects(pt_scene* s, const pt_object* objs, int64_t first, int64_t n) {
     if (!s || first < 0 || n < 0 || first > s->nobj || n > s->nobj - first || (n > 0 && !objs))
         return fail(PT_ERR_INVALID, "pt_scene_update_objects: bad argument");
+    if (s->instanced) return fail(PT_ERR_INVALID, "pt_scene_update_objects: not for instanced scenes");
     for (int64_t i = 0; i < n; i++) {
         if (objs[i].type != PT_SPHERE && objs[i].type != PT_TRIANGLE)
             return fail(PT_ERR_INVALID, "pt_scene_update_objects: unknown object type");
@@ -2575,6 +2992,10 @@ int pt_scene_build_bvh_ex(pt_scene* s, int flags, void* stream) {
     if (!s) return fail(PT_ERR_INVALID, "pt_scene_build_bvh: null scene");
     int rc = setDevice(s->device);
     if (rc) return rc;
+    if (s->instanced) {   // the two-level tree, on the host (flags: the LBVH's, not applicable)
+        s->built = false;
+        return buildInstanced(s);
+    }
     const int64_t n = s->nobj;
     s->built = false;
     s->wideReady = false;   // the wide buffers are kept for the next wide build
@@ -2746,6 +3167,7 @@ int pt_scene_bvh_info(pt_scene* s, int* depth, int64_t* nodes, int64_t* bytes) {
 int pt_scene_download_bvh(pt_scene* s, pt_bvh_node* out) {
     if (!s || !out) return fail(PT_ERR_INVALID, "pt_scene_download_bvh: null argument");
     if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
+    if (s->instanced) return fail(PT_ERR_STATE, "pt_scene_download_bvh: an instanced scene has no LBVH");
     int rc = setDevice(s->device);
     if (rc) return rc;
     const int64_t n = s->nobj;
@@ -2812,7 +3234,9 @@ int traceDevice(pt_scene* s, const pt_ray* dr, int64_t n, float tmin, float tmax
     if (!s->built) return fail(PT_ERR_STATE, "BVH not built");
     int rc = setDevice(s->device);
     if (rc) return rc;
-    const bool wide = kernel == PT_KERNEL_WIDE;
+    const bool wide = kernel == PT_KERNEL_WIDE || s->instanced;
+    if (s->instanced && kernel != PT_KERNEL_DEFAULT && kernel != PT_KERNEL_WIDE)
+        return fail(PT_ERR_INVALID, "pt_trace_closest: instanced scenes trace with the wide kernel");
     if (wide && (rc = ensureWide(s))) return rc;
     const int stack = wide ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
     StreamGuard guard(st);
@@ -2981,6 +3405,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     }
     if (kernel != PT_KERNEL_SIMPLE && kernel != PT_KERNEL_WAVEFRONT && kernel != PT_KERNEL_WIDE)
         return fail(PT_ERR_INVALID, "pt_render_ex: unknown kernel");
+    if (s->instanced && kernel != PT_KERNEL_WIDE)
+        return fail(PT_ERR_INVALID, "pt_render_ex: instanced scenes render with the wide kernel (PT_KERNEL_WIDE)");
     const int rng = opts ? opts->rng : PT_RNG_COMPAT;
     if (rng != PT_RNG_COMPAT && rng != PT_RNG_SAMPLE) return fail(PT_ERR_INVALID, "pt_render_ex: unknown rng mode");
     if (kernel == PT_KERNEL_WIDE && (rc = ensureWide(s))) return rc;   // (first use: builds the tree)
@@ -3092,7 +3518,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         // persistent: exactly the waves that fit at once (the kernel's occupancy per CU, which
         // the LDS stack caps below PT_WAVES_PER_EU per SIMD on deep trees)
         int perCU = 0;
-        if ((rc = persistentWavesPerCU(stack, kernel, perCU))) return rc;
+        if ((rc = persistentWavesPerCU(stack, kernel, perCU, s->instanced))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
         // Tile costs (rays of the tile's most expensive pixel) are measured on the first frame and

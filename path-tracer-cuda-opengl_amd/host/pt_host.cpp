@@ -460,6 +460,79 @@ int pt_camera_move(pt_camera* c, int dir, float dt) {
     return PT_OK;
 }
 
+int pt_preset_instanced(const char* name, const char* models_dir, int width, int height, pt_instanced_desc* out) {
+    if (!name || !out) return fail(PT_ERR_INVALID, "pt_preset_instanced: null argument");
+    std::memset(out, 0, sizeof(*out));
+    const std::string n = name, dir = models_dir ? models_dir : "models";
+    if (n != "bunny_field" && n != "bunny_cornell" && n != "cornell")
+        return fail(PT_ERR_INVALID, "pt_preset_instanced: no instanced form of '" + n + "'");
+    try {
+        // the flat preset for the frame, camera and materials; the meshes rebuilt in object space
+        Scene flat = buildPreset(n, dir, width, height);
+        Scene box, bunny;
+        cornellBox(box, dir);   // (its own materials: the same 3 as the flat preset's first ones)
+        std::vector<pt_instance> inst;
+        auto translate = [](float x, float y, float z, int mesh) {
+            pt_instance i{};
+            i.m[0] = 1.0f; i.m[5] = 1.0f; i.m[10] = 1.0f;
+            i.m[3] = x; i.m[7] = y; i.m[11] = z;
+            i.mesh = mesh;
+            return i;
+        };
+        inst.push_back(translate(0.0f, 0.0f, 0.0f, 0));   // the box, identity
+        if (n == "bunny_cornell") {
+            appendObj(bunny, dir + "/bunny/bunny.obj", 1500.0f, vec3(0, 0, 0), 0);
+            inst.push_back(translate(438.0f, -49.96f, 113.0f, 1));
+        } else if (n == "bunny_field") {   // pt_preset_scene's 15 x 14 grid, same order
+            appendObj(bunny, dir + "/bunny/bunny.obj", 250.0f, vec3(0, 0, 0), 0);
+            for (int i = 0; i < 15; i++)
+                for (int j = 0; j < 14; j++)
+                    inst.push_back(translate(24.0f + 35.5f * (float)i, -8.33f, 16.0f + 38.0f * (float)j, 1));
+        }
+        std::vector<pt_object> objs = box.objects;
+        objs.insert(objs.end(), bunny.objects.begin(), bunny.objects.end());
+        const int nm = bunny.objects.empty() ? 1 : 2;
+        out->n_objects = (int64_t)objs.size();
+        out->objects = (pt_object*)std::malloc(sizeof(pt_object) * std::max<size_t>(1, objs.size()));
+        out->n_meshes = nm;
+        out->mesh_first = (int64_t*)std::malloc(sizeof(int64_t) * 2);
+        out->mesh_count = (int64_t*)std::malloc(sizeof(int64_t) * 2);
+        out->n_instances = (int64_t)inst.size();
+        out->instances = (pt_instance*)std::malloc(sizeof(pt_instance) * inst.size());
+        out->n_materials = (int64_t)flat.materials.size();
+        out->materials = (pt_material*)std::malloc(sizeof(pt_material) * std::max<size_t>(1, flat.materials.size()));
+        if (!out->objects || !out->mesh_first || !out->mesh_count || !out->instances || !out->materials)
+            return fail(PT_ERR_NOMEM, "pt_preset_instanced: out of memory");
+        std::memcpy(out->objects, objs.data(), sizeof(pt_object) * objs.size());
+        out->mesh_first[0] = 0;
+        out->mesh_count[0] = (int64_t)box.objects.size();
+        out->mesh_first[1] = (int64_t)box.objects.size();
+        out->mesh_count[1] = (int64_t)bunny.objects.size();
+        std::memcpy(out->instances, inst.data(), sizeof(pt_instance) * inst.size());
+        std::memcpy(out->materials, flat.materials.data(), sizeof(pt_material) * flat.materials.size());
+        out->camera = flat.cam;
+        out->width = flat.width;
+        out->height = flat.height;
+        out->spp = flat.spp;
+        out->max_depth = flat.max_depth;
+        std::snprintf(out->name, sizeof(out->name), "%s", flat.name.c_str());
+    } catch (const std::exception& e) {
+        pt_instanced_desc_free(out);
+        return fail(PT_ERR_IO, std::string("pt_preset_instanced: ") + e.what());
+    }
+    return PT_OK;
+}
+
+void pt_instanced_desc_free(pt_instanced_desc* d) {
+    if (!d) return;
+    std::free(d->objects);
+    std::free(d->mesh_first);
+    std::free(d->mesh_count);
+    std::free(d->instances);
+    std::free(d->materials);
+    std::memset(d, 0, sizeof(*d));
+}
+
 int pt_preset_scene(const char* name, const char* models_dir, int width, int height, pt_scene_desc* out) {
     if (!name || !out) return fail(PT_ERR_INVALID, "pt_preset_scene: null argument");
     std::memset(out, 0, sizeof(*out));

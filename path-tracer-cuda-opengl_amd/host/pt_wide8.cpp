@@ -222,6 +222,61 @@ std::vector<uint32_t> referenceRanks(const uint32_t* leftRef, const uint32_t* ri
 
 bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
                 std::string& err) {
+    return buildWide8Leaf(prims, boxes, rank, n, envLeaf(), out, err);
+}
+
+void relocateWide8(Wide8& w, uint32_t nodeBase, uint32_t primBase) {
+    for (size_t s = 0; s < w.nodes.size(); s += kW8NodeDwords) {
+        w.nodes[s + 4] += nodeBase;
+        w.nodes[s + 5] += primBase;
+    }
+}
+
+bool instanceLeaves(Wide8& top, uint32_t (*instanceOf)(const uint32_t* primRecord),
+                    void (*record)(uint32_t id, uint32_t* dst, void* ctx), void* ctx, std::string& err) {
+    const size_t nodes0 = top.nodes.size() / kW8NodeDwords;
+    for (size_t s = 0; s < nodes0; s++) {
+        uint32_t* R = &top.nodes[s * kW8NodeDwords];
+        if (R[3] == kW8InstanceFlag) continue;
+        uint8_t meta[8];
+        for (int j = 0; j < 8; j++) meta[j] = (uint8_t)((j < 4 ? R[6] : R[7]) >> (8 * (j & 3)));
+        bool anyInternal = false, anyLeaf = false;
+        for (int j = 0; j < 8; j++) {
+            if (!meta[j]) continue;
+            if ((meta[j] & 0x1f) >= 24) anyInternal = true;
+            else anyLeaf = true;
+        }
+        if (!anyLeaf) continue;
+        if (!anyInternal) {   // no child block yet: one for the instance records
+            R[4] = (uint32_t)(top.nodes.size() / kW8NodeDwords);
+            top.nodes.resize(top.nodes.size() + 8 * (size_t)kW8NodeDwords, 0u);
+            R = &top.nodes[s * kW8NodeDwords];
+        }
+        if ((int64_t)R[4] + 8 > ((int64_t)1 << 24)) {
+            err = "instanced BVH: more than 2^24 node slots";
+            return false;
+        }
+        for (int j = 0; j < 8; j++) {
+            if (!meta[j] || (meta[j] & 0x1f) >= 24) continue;
+            if ((meta[j] >> 5) != 1u) {
+                err = "instanced BVH: top-level leaf with more than one instance";
+                return false;
+            }
+            const uint32_t prim = R[5] + (meta[j] & 0x1fu);
+            const uint32_t id = instanceOf(&top.prims[(size_t)prim * kW8PrimDwords]);
+            record(id, &top.nodes[(size_t)(R[4] + (uint32_t)j) * kW8NodeDwords], ctx);
+            meta[j] = (uint8_t)(0x20 | 24 | j);   // an internal child: its slot holds the instance
+            top.usedNodes++;
+        }
+        R[6] = (uint32_t)meta[0] | (uint32_t)meta[1] << 8 | (uint32_t)meta[2] << 16 | (uint32_t)meta[3] << 24;
+        R[7] = (uint32_t)meta[4] | (uint32_t)meta[5] << 8 | (uint32_t)meta[6] << 16 | (uint32_t)meta[7] << 24;
+    }
+    top.prims.clear();   // (the top level has no primitives left)
+    return true;
+}
+
+bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, int maxLeaf,
+                    Wide8& out, std::string& err) {
     out = Wide8{};
     if (n <= 0) return true;
     if (n >= (int64_t)1 << 26) {
@@ -229,7 +284,7 @@ bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank,
         return false;
     }
     SahBuilder B;
-    B.kMaxLeaf = envLeaf();
+    B.kMaxLeaf = std::max(1, std::min(3, maxLeaf));
     B.kTravCost = envTrav();
     B.boxes = reinterpret_cast<const BBox*>(boxes);
     B.cen.resize((size_t)n * 3);

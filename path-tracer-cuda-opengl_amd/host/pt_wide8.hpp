@@ -32,6 +32,26 @@ struct Wide8 {
 // limits.
 bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
                 std::string& err);
+// buildWide8 with at most maxLeaf (1..3) primitives per leaf child (instancing's top level: one
+// instance per leaf).
+bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, int maxLeaf,
+                    Wide8& out, std::string& err);
+
+// Instancing (two-level tree in one node array).  Record of an instance node, kW8NodeDwords:
+//   [0] 1 if the transform is the identity (the ray is not transformed), [1..2] 0,
+//   [3] kW8InstanceFlag (never a valid exponent word: byte 3 of a node's exponents is 0),
+//   [4] the instance's bottom-level root slot, [5] the instance id, [6..7] 0,
+//   [8..19] the world-to-object transform, 3 rows of {m0, m1, m2, t} (fp32).
+constexpr uint32_t kW8InstanceFlag = 0xff000000u;
+// Relocate a tree built on its own into a shared node / primitive array: child bases += nodeBase,
+// primitive bases += primBase.
+void relocateWide8(Wide8& w, uint32_t nodeBase, uint32_t primBase);
+// Turn the leaf children of a top-level tree built with buildWide8Leaf(.., 1, ..) over instance
+// boxes into internal children whose slots hold instance records: instanceOf(prim record) gives
+// the instance id of a leaf's primitive record, record(id, dst) writes its 20-dword record.
+// Nodes without a child block get one.  Returns false with err set past the encoding limits.
+bool instanceLeaves(Wide8& top, uint32_t (*instanceOf)(const uint32_t* primRecord),
+                    void (*record)(uint32_t id, uint32_t* dst, void* ctx), void* ctx, std::string& err);
 
 // The order in which RenderManager::hitBvh (render_manager.h:105-133) would test the leaves of
 // the binary LBVH if every box passed: at a node, its leaf children (left, then right), then the

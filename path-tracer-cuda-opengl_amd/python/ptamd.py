@@ -69,6 +69,17 @@ class SceneDesc(C.Structure):
                 ("spp", C.c_int32), ("max_depth", C.c_int32), ("name", C.c_char * 64)]
 
 
+INSTANCE_DTYPE = np.dtype([("m", np.float32, 12), ("mesh", np.int32), ("reserved", np.int32)])
+
+
+class InstancedDesc(C.Structure):
+    _fields_ = [("objects", C.c_void_p), ("n_objects", C.c_int64), ("mesh_first", C.c_void_p),
+                ("mesh_count", C.c_void_p), ("n_meshes", C.c_int32), ("instances", C.c_void_p),
+                ("n_instances", C.c_int64), ("materials", C.c_void_p), ("n_materials", C.c_int64),
+                ("camera", Camera), ("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
+                ("max_depth", C.c_int32), ("name", C.c_char * 64)]
+
+
 # Every symbol include/pt.h declares (checked by the CPU tests).
 EXPORTS = [
     "pt_last_error", "pt_abi_version", "pt_device_count", "pt_camera_make", "pt_camera_move",
@@ -78,7 +89,8 @@ EXPORTS = [
     "pt_render", "pt_render_ex", "pt_film_reset", "pt_film_destroy", "pt_scene_destroy",
     "pt_film_clear", "pt_film_accumulated", "pt_write_png_rgba8", "pt_scene_build_time",
     "pt_scene_update_objects", "pt_trace_closest_ex", "pt_scene_wide_info", "pt_trace_closest_device",
-    "pt_scene_build_bvh_ex", "pt_film_stats",
+    "pt_scene_build_bvh_ex", "pt_film_stats", "pt_preset_instanced", "pt_instanced_desc_free",
+    "pt_scene_create_instanced",
 ]
 
 if not os.path.exists(LIB_PATH):
@@ -102,6 +114,10 @@ _sig = {
     "pt_quantize_rgba8": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "pt_scene_create": (C.c_int, [C.c_int, _P, C.c_int64, _P, C.c_int64, C.POINTER(C.c_void_p)]),
     "pt_scene_build_bvh": (C.c_int, [_P, C.c_int]),
+    "pt_preset_instanced": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.POINTER(InstancedDesc)]),
+    "pt_instanced_desc_free": (None, [C.POINTER(InstancedDesc)]),
+    "pt_scene_create_instanced": (C.c_int, [C.c_int, _P, C.c_int64, _P, _P, C.c_int, _P, C.c_int64, _P, C.c_int64,
+                                            C.POINTER(C.c_void_p)]),
     "pt_scene_build_bvh_ex": (C.c_int, [_P, C.c_int, _P]),
     "pt_film_stats": (C.c_int, [_P, C.POINTER(Stats)]),
     "pt_scene_build_time": (C.c_int, [_P, C.POINTER(C.c_double)]),
@@ -194,6 +210,35 @@ class Preset:
             lib.pt_scene_desc_free(C.byref(d))
 
 
+def _copy_array(ptr, n, dtype):
+    if not n:
+        return np.zeros(0, dtype)
+    return np.frombuffer(bytes((C.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)), dtype=dtype).copy()
+
+
+class InstancedPreset:
+    """pt_preset_instanced: meshes (object ranges, object space) placed by instance transforms."""
+
+    def __init__(self, name: str, width: int = 0, height: int = 0, models_dir: str = MODELS_DIR):
+        d = InstancedDesc()
+        _check(lib.pt_preset_instanced(name.encode(), models_dir.encode(), width, height, C.byref(d)),
+               "pt_preset_instanced")
+        try:
+            self.objects = _copy_array(d.objects, d.n_objects, OBJECT_DTYPE)
+            self.mesh_first = _copy_array(d.mesh_first, d.n_meshes, np.int64)
+            self.mesh_count = _copy_array(d.mesh_count, d.n_meshes, np.int64)
+            self.instances = _copy_array(d.instances, d.n_instances, INSTANCE_DTYPE)
+            self.materials = _copy_array(d.materials, d.n_materials, MATERIAL_DTYPE)
+            self.camera = Camera.from_buffer_copy(bytes(d.camera))
+            self.width, self.height, self.spp, self.max_depth = d.width, d.height, d.spp, d.max_depth
+            self.name = d.name.decode()
+        finally:
+            lib.pt_instanced_desc_free(C.byref(d))
+
+    def flattened_count(self) -> int:
+        return int(sum(self.mesh_count[i["mesh"]] for i in self.instances))
+
+
 def load_obj(path: str, scale: float = 1.0, translate=(0.0, 0.0, 0.0), mat: int = 0) -> np.ndarray:
     out = C.c_void_p()
     n = C.c_int64()
@@ -248,6 +293,32 @@ class Scene:
         self.h = h
         if build:
             self.build_bvh(flags)
+
+    @classmethod
+    def instanced(cls, objects: np.ndarray, mesh_first, mesh_count, instances: np.ndarray, materials: np.ndarray,
+                  device: int = 0, build: bool = True) -> "Scene":
+        """pt_scene_create_instanced: each mesh stored once (object space), placed by `instances`
+        (INSTANCE_DTYPE); rendered and traced by the wide kernel over a two-level tree."""
+        self = cls.__new__(cls)
+        self.objects = np.ascontiguousarray(objects, OBJECT_DTYPE)
+        self.materials = np.ascontiguousarray(materials, MATERIAL_DTYPE)
+        self.mesh_first = np.ascontiguousarray(mesh_first, np.int64)
+        self.mesh_count = np.ascontiguousarray(mesh_count, np.int64)
+        self.instances = np.ascontiguousarray(instances, INSTANCE_DTYPE)
+        self.device = device
+        self.h = None
+        h = C.c_void_p()
+        _check(lib.pt_scene_create_instanced(
+            device, _ptr(self.objects) if len(self.objects) else None, len(self.objects),
+            _ptr(self.mesh_first) if len(self.mesh_first) else None,
+            _ptr(self.mesh_count) if len(self.mesh_count) else None, len(self.mesh_first),
+            _ptr(self.instances) if len(self.instances) else None, len(self.instances),
+            _ptr(self.materials) if len(self.materials) else None, len(self.materials), C.byref(h)),
+            "pt_scene_create_instanced")
+        self.h = h
+        if build:
+            self.build_bvh()
+        return self
 
     def build_bvh(self, flags: int = PT_BVH_ORIGIN_BOUNDS, stream=None) -> None:
         """pt_scene_build_bvh_ex: the build's device work on `stream` (a hipStream_t handle or None)."""

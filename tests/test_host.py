@@ -167,3 +167,39 @@ def test_device_calls_fail_loudly_without_gpu(pt):
     with pytest.raises(pt.PtError) as e:
         pt.Scene(p.objects, p.materials)
     assert e.value.code == 5   # PT_ERR_NODEVICE: no CPU fallback
+
+
+@pytest.mark.parametrize("name", ["cornell", "bunny_cornell", "bunny_field"])
+def test_instanced_presets_flatten_to_the_flat_presets(pt, name):
+    """pt_preset_instanced: meshes once in object space + translations; written out in instance
+    order they are pt_preset_scene's objects bit for bit (v_world = v_object + t in float)."""
+    ip, fp = pt.InstancedPreset(name), pt.Preset(name)
+    parts = []
+    for inst in ip.instances:
+        m = inst["m"].reshape(3, 4)
+        np.testing.assert_array_equal(m[:, :3], np.eye(3, dtype=np.float32))
+        f, c = ip.mesh_first[inst["mesh"]], ip.mesh_count[inst["mesh"]]
+        o = ip.objects[f:f + c].copy()
+        o["v"] = (o["v"].reshape(-1, 3, 3) + m[:, 3]).reshape(-1, 9)
+        parts.append(o)
+    flat = np.concatenate(parts)
+    assert ip.flattened_count() == len(fp.objects) == len(flat)
+    np.testing.assert_array_equal(flat["v"], fp.objects["v"])
+    np.testing.assert_array_equal(flat["mat"], fp.objects["mat"])
+    np.testing.assert_array_equal(ip.materials, fp.materials)
+    assert bytes(ip.camera) == bytes(fp.camera)
+    if name == "bunny_field":
+        assert len(ip.instances) == 211 and len(ip.objects) == 32 + 4968
+
+
+def test_instanced_scene_argument_checks(pt):
+    """pt_scene_create_instanced rejects bad meshes and instances before touching a device."""
+    ip = pt.InstancedPreset("bunny_cornell")
+    bad = ip.instances.copy()
+    bad["mesh"][0] = 7
+    for first, count, inst in ((ip.mesh_first, ip.mesh_count, bad),
+                               (ip.mesh_first, ip.mesh_count + 1, ip.instances),
+                               (ip.mesh_first, ip.mesh_count, ip.instances[:0])):
+        with pytest.raises(pt.PtError) as e:
+            pt.Scene.instanced(ip.objects, first, count, inst, ip.materials)
+        assert e.value.code == 1   # PT_ERR_INVALID
