@@ -10,7 +10,9 @@
 //
 // Deliberate, documented deviations from the reference:
 //  * camera lens/time draws come from the shared state[0] in the reference (main.cu:286, a
-//    cross-thread race); with aperture 0 they have no geometric effect and are skipped.
+//    cross-thread race, not reproducible).  The time draw has no effect (no moving objects) and
+//    is skipped; a lens radius > 0 draws its disk sample from the path's own stream after u, v
+//    (cameraRay); a pinhole camera (every BASELINE scene) draws nothing.
 //  * reflectance()'s powf(x, 5) (physical.h:24) is evaluated as ((x*x)*(x*x))*x.
 //  * tight internal BVH boxes (the reference seeds them with the origin, bvh.h:124-127); the
 //    reference-inflated variant is available (tight=0) to show the hits are unchanged.
@@ -643,6 +645,28 @@ int orc_render(const orc_object* objs, int64_t nobj, const orc_material* mats, i
 }  // extern "C"
 
 namespace {
+// camera::get_ray's lens sample (camera.h:58-62).  The reference draws it in polar form
+// (utility.h:98-102) from the shared randState[0] (main.cu:286, raced by all threads: not
+// reproducible); restated as the kernels draw it: from the path's own stream after u, v, a uniform
+// point of the unit disk by rejection, scaled by the lens radius, along right / up.  Pinhole
+// cameras (lens radius 0, every BASELINE scene) draw nothing.
+template <class R>
+Ray cameraRay(const orc_camera* cam, V3 pos, V3 ll, V3 hor, V3 ver, float u, float v, R& rng) {
+    Ray r{pos, ((ll + u * hor) + v * ver) - pos};
+    if (cam->lens_radius != 0.0f) {
+        float x, y;
+        do {
+            x = 2.0f * (rng() - 0.5f);
+            y = 2.0f * (rng() - 0.5f);
+        } while (x * x + y * y >= 1.0f);
+        const float rx = cam->lens_radius * x, ry = cam->lens_radius * y;
+        const V3 off = rx * load3(cam->right) + ry * load3(cam->up);
+        r.o = r.o + off;
+        r.d = r.d - off;
+    }
+    return r;
+}
+
 // One camera sample of pixel (col, row): main.cu:284-288 (rng draws u, v, then the bounces).
 template <class R>
 V3 tracePath(const orc_object* objs, int64_t nobj, const orc_material* mats, const orc_node* nodes, const orc_camera* cam,
@@ -651,7 +675,7 @@ V3 tracePath(const orc_object* objs, int64_t nobj, const orc_material* mats, con
     const V3 hor = load3(cam->horizontal), ver = load3(cam->vertical);
     float u = ((float)col + rng()) * invW;
     float v = ((float)row + rng()) * invH;
-    Ray cur{pos, ((ll + u * hor) + v * ver) - pos};
+    Ray cur = cameraRay(cam, pos, ll, hor, ver, u, v, rng);
     local.paths++;
     V3 att{1, 1, 1};
     int depth = max_depth;
@@ -706,7 +730,7 @@ int orc_render3(const orc_object* objs, int64_t nobj, const orc_material* mats, 
                 for (int i = 0; i < spp; i++) {                                        // main.cu:283-289
                     float u = ((float)col + curandUniform(s)) * invW;
                     float v = ((float)row + curandUniform(s)) * invH;
-                    Ray r{pos, ((ll + u * hor) + v * ver) - pos};                      // camera.h:58-64
+                    Ray r = cameraRay(cam, pos, ll, hor, ver, u, v, rng);              // camera.h:58-64
                     local.paths++;
                     // rayTracing, main.cu:21-37
                     V3 att{1, 1, 1};

@@ -88,7 +88,10 @@ constexpr uint32_t kInstFlag = 0xff000000u;
 
 struct DevCamera {
     float3 pos, ll, hor, ver;
+    float3 right, up;
+    float lens;   // lens radius (aperture / 2); 0: a pinhole, no lens draws
 };
+
 
 struct Counters {
     uint32_t rays, visits, tris, spheres;
@@ -877,6 +880,25 @@ __device__ __forceinline__ void waveReduceAdd(unsigned long long* dst, uint32_t 
 // SAMPLE: the sample-mode streams and block sums, one wave per tile, samples in order -- the
 // same frame as renderKernelWF<STACK, true>, in the reference's traversal order (the bench
 // counts algorithmic bytes with it).
+// Lens sample of camera::get_ray (camera.h:58-62): a uniform point of the unit disk scaled by the
+// lens radius, offset along right / up.  The reference draws it in polar form (utility.h:98-102:
+// sqrtf, cosf, sinf) from the SHARED state randState[0] (main.cu:286, raced by every thread), so
+// its lens samples are not reproducible; here they come from the path's own stream, right after
+// the pixel jitter, by rejection (x, y in [-1, 1) until x^2 + y^2 < 1: the same uniform disk, and
+// no transcendental, so the oracle's arithmetic is the kernel's bit for bit).
+template <class G>
+__device__ __forceinline__ void lensOffset(float3 right, float3 up, float lens, G& g, float3& o, float3& d) {
+    float x, y;
+    do {
+        x = 2.0f * (g.uniform() - 0.5f);
+        y = 2.0f * (g.uniform() - 0.5f);
+    } while (x * x + y * y >= 1.0f);
+    const float rx = lens * x, ry = lens * y;
+    const float3 off = add(scale(rx, right), scale(ry, up));
+    o = add(o, off);
+    d = sub(d, off);
+}
+
 template <int STACK, bool SAMPLE>
 __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
     __shared__ uint32_t stk[STACK * kWave];
@@ -899,13 +921,15 @@ __global__ __launch_bounds__(kWave) void renderKernel(RenderParams P) {
         float3 sum = f3(0.0f, 0.0f, 0.0f);
         float3 o, d, att;
         int depthLeft = 0, sample = 0;
-        // newPath: main.cu:284-286 + camera::get_ray (camera.h:58-64), lens/time draws skipped.
+        // newPath: main.cu:284-286 + camera::get_ray (camera.h:58-64): the lens sample from the
+        // path's stream (lensOffset), the time draw skipped (no moving objects on the path).
         auto newPath = [&]() {
             if constexpr (SAMPLE) g = sampleStream(P.seed0, P.seed1, P.sampleBase + (uint32_t)sample, gpix);
             float u = (fcol + g.uniform()) * P.invW;
             float v = (frow + g.uniform()) * P.invH;
             o = P.cam.pos;
             d = sub(add(add(P.cam.ll, scale(u, P.cam.hor)), scale(v, P.cam.ver)), P.cam.pos);
+            if (P.cam.lens != 0.0f) lensOffset(P.cam.right, P.cam.up, P.cam.lens, g, o, d);
             att = f3(1.0f, 1.0f, 1.0f);
             depthLeft = P.max_depth;
             paths++;
@@ -1185,7 +1209,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             node = 0;                                                                             \
         }                                                                                         \
     } while (0)
-    // New camera sample: main.cu:284-286 + camera::get_ray (lens/time draws skipped).
+    // New camera sample: main.cu:284-286 + camera::get_ray (lens sample: lensOffset; time draw skipped).
     // Sample mode: lanes with needTask take the next tasks of the wave's pool, in lane order; an
     // empty pool is refilled with the next kTaskPool tasks of the global counter (one returning
     // atomic, whose latency the wave waits out, per kTaskPool tasks instead of per SHADE step).
@@ -1269,6 +1293,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         const float v_ = (frow + g.uniform()) * Q_.invH;                                           \
         o = ld3(Q_.cam.pos);                                                                            \
         d = sub(add(add(ld3(Q_.cam.ll), scale(u_, ld3(Q_.cam.hor))), scale(v_, ld3(Q_.cam.ver))), ld3(Q_.cam.pos));       \
+        if (Q_.cam.lens != 0.0f) lensOffset(ld3(Q_.cam.right), ld3(Q_.cam.up), Q_.cam.lens, g, o, d); \
         att = f3(1.0f, 1.0f, 1.0f);                                                               \
         depthLeft = Q_.max_depth;                                                                  \
     } while (0)
@@ -3381,9 +3406,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     if (!s || !f || !cam || !out || spp <= 0) return fail(PT_ERR_INVALID, "pt_render: bad argument");
     if (!s->built) return fail(PT_ERR_STATE, "pt_render: BVH not built");
     if (s->device != f->device) return fail(PT_ERR_INVALID, "pt_render: scene and film on different devices");
-    if (cam->lens_radius != 0.0f)
-        return fail(PT_ERR_INVALID, "pt_render: aperture > 0 is not supported (reference draws the lens sample "
-                                    "from a shared racy stream, main.cu:286)");
+    if (!(cam->lens_radius >= 0.0f) || !std::isfinite(cam->lens_radius))
+        return fail(PT_ERR_INVALID, "pt_render: lens radius must be finite and >= 0");
     int rc = setDevice(s->device);
     if (rc) return rc;
     hipStream_t st = on_dev ? (hipStream_t)stream : 0;
@@ -3434,6 +3458,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.cam.ll = make_float3(cam->lower_left[0], cam->lower_left[1], cam->lower_left[2]);
     P.cam.hor = make_float3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
     P.cam.ver = make_float3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
+    P.cam.right = make_float3(cam->right[0], cam->right[1], cam->right[2]);
+    P.cam.up = make_float3(cam->up[0], cam->up[1], cam->up[2]);
+    P.cam.lens = cam->lens_radius;
     uint32_t* b = f->state.as<uint32_t>();
     P.sd = b; P.s0 = b + np; P.s1 = b + 2 * np; P.s2 = b + 3 * np; P.s3 = b + 4 * np; P.s4 = b + 5 * np;
     P.out = static_cast<float*>(dst);
@@ -3469,7 +3496,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     {   // wideFar (pt_device.hip) for the camera: its rays then take the reference-order path
         const float m = std::fmax(std::fmax(std::fabs(cam->origin[0] - s->sceneCE[0]), std::fabs(cam->origin[1] - s->sceneCE[1])),
                                   std::fabs(cam->origin[2] - s->sceneCE[2]));
-        P.camFar = !(m <= 8.0f * s->sceneCE[3]) ? 1 : 0;
+        // (+ the lens: camera ray origins lie within 1.5 lens radii of the camera, per axis)
+        P.camFar = !(m + 1.5f * cam->lens_radius <= 8.0f * s->sceneCE[3]) ? 1 : 0;
     }
     // Defaults swept on C3 (tools/ab_env.py): sample mode is throughput-bound and prefers full
     // LEAF / SHADE steps.  Compat mode is bound by its slowest pixels' sequential chains: 20 / 12

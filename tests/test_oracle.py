@@ -228,3 +228,99 @@ def test_sample_mode_statistical_parity(pt, orc):
     assert sa.rays == sb.rays and sa.tri_tests == sb.tri_tests
     np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6)
     np.testing.assert_array_equal(a, rgb.reshape(675, 1200, 3)[small].reshape(-1, 3))
+
+
+# --- the reference's committed chapter renders (output/*.png) -----------------------------------
+# The project was built through the RTIOW chapters; those chapters' scene code is gone from the
+# reference (only the images remain), so the scenes are restated here from the chapters: spheres
+# (centre, radius, material), material = (type, albedo, fuzz, ir) with type 1 lambertian, 2 metal,
+# 4 dielectric.  Where a chapter leaves a value open (the metal fuzz, the hollow glass sphere),
+# the value is the one of {0, 0.1, 0.3, 1} x {solid, -0.4, -0.45} that matches; the negative
+# controls below show that the block-mean statistic separates such variants.
+def _lam(a):
+    return (1, a, 0.0, 0.0)
+
+
+def _met(a, f):
+    return (2, a, f, 0.0)
+
+
+_GLASS = (4, (0, 0, 0), 0.0, 1.5)
+_GROUND_Y = ((0, -100.5, -1), 100.0)
+CHAPTERS = {
+    # diffuse: gray spheres, the reference's current lambertian (material.h:32, randomOnUnitSphere)
+    "c8_sampleOnSphere": [((0, 0, -1), 0.5, _lam((0.5,) * 3)), (*_GROUND_Y, _lam((0.5,) * 3))],
+    # metal
+    "c9": [(*_GROUND_Y, _lam((0.8, 0.8, 0.0))), ((0, 0, -1), 0.5, _lam((0.7, 0.3, 0.3))),
+           ((-1, 0, -1), 0.5, _met((0.8, 0.8, 0.8), 0.0)), ((1, 0, -1), 0.5, _met((0.8, 0.6, 0.2), 1.0))],
+    # dielectric: a hollow glass sphere (negative inner radius flips its normals)
+    "c10": [(*_GROUND_Y, _lam((0.8, 0.8, 0.0))), ((0, 0, -1), 0.5, _lam((0.1, 0.2, 0.5))),
+            ((-1, 0, -1), 0.5, _GLASS), ((-1, 0, -1), -0.4, _GLASS), ((1, 0, -1), 0.5, _met((0.8, 0.6, 0.2), 1.0))],
+}
+CHAPTERS["c11"] = CHAPTERS["c10"]
+# the final scene's big spheres and ground: the reference's own main.cu:231-242 values
+FINAL = [((0, -1000, 0), 1000.0, _lam((0.5, 0.5, 0.5))), ((4, 1, 0), 1.0, _GLASS), ((4, 1, 0), -0.9, _GLASS),
+         ((-4, 1, 0), 1.0, _lam((1, 0, 0.4))), ((0, 1, 0), 1.0, _met((0.7, 0.6, 0.5), 0.0))]
+
+
+def _spheres(spheres):
+    from helpers import MATERIAL_DTYPE, OBJECT_DTYPE
+    objs = np.zeros(len(spheres), OBJECT_DTYPE)
+    mats = np.zeros(len(spheres), MATERIAL_DTYPE)
+    for k, (c, r, m) in enumerate(spheres):
+        objs[k]["type"] = 1
+        objs[k]["v"][:3] = c
+        objs[k]["v"][3] = r
+        objs[k]["mat"] = k
+        mats[k]["type"], mats[k]["albedo"], mats[k]["fuzz"], mats[k]["ir"] = m
+    return objs, mats
+
+
+def _blocks(orc, spheres, cam, w, h, spp=6, block=25):
+    objs, mats = _spheres(spheres)
+    rows = np.arange(h, dtype=np.int32)
+    rgb, _ = orc.render_sample(objs, mats, orc.build_lbvh(objs, orc.morton_keys(objs)), cam, w, h, rows, spp, 50, 3,
+                               chunk=16, nthreads=os.cpu_count() or 4)
+    return (rgb.astype(np.float64) ** 2).reshape(h // block, block, w // block, block, 3).mean(axis=(1, 3))
+
+
+def _chapter_camera(orc, key):
+    if key == "c11":   # defocus blur: lookfrom (3,3,2) at (0,0,-1), vfov 20, aperture 2, focus |from - at|
+        return orc.camera_make((3, 3, 2), (0, 0, -1), 20.0, 2.0, 2.0, float(np.sqrt(27.0)))
+    return orc.camera_make((0, 0, 0), (0, 0, -1), 90.0, 2.0)   # viewport 4 x 2 at focal length 1
+
+
+@pytest.mark.parametrize("key", ["c8_sampleOnSphere", "c9", "c10", "c11"])
+def test_reference_chapter_renders(orc, key):
+    """Oracle renders of the chapter scenes at 1200x600 vs the reference's committed PNGs
+    (linear 25x25 block means; measured at 8 spp: 0.0010-0.0014 mean, 0.008-0.02 max)."""
+    ref = np.load(os.path.join(GOLDEN, "chapter_blocks.npz"))[key]
+    d = np.abs(_blocks(orc, CHAPTERS[key], _chapter_camera(orc, key), 1200, 600) - ref)
+    assert d.mean() < 0.003 and d.max() < 0.04, (d.mean(), d.max())
+
+
+def test_reference_final_scene_consensus_blocks(orc):
+    """output/13*.png: the final scene (random small spheres differ per image) on the blocks where
+    all three renders agree -- sky and the three big spheres: camera (13,2,3) -> 0, vfov 20,
+    aperture 0.1, focus 10, and the big spheres of main.cu:231-242 (hollow glass, (1, 0, 0.4))."""
+    g = np.load(os.path.join(GOLDEN, "chapter_blocks.npz"))
+    cons, ref = g["c13_consensus"], g["c13_mean"]
+    assert cons.sum() > 250
+    cam = orc.camera_make((13, 2, 3), (0, 0, 0), 20.0, 1.5, 0.1, 10.0)
+    d = np.abs(_blocks(orc, FINAL, cam, 1200, 800) - ref)[cons]
+    # measured at 8 spp: 0.0019 mean, 0.016 max (solid glass: 0.026 / 0.55)
+    assert d.mean() < 0.004 and d.max() < 0.04, (d.mean(), d.max())
+
+
+def test_chapter_statistic_separates_variants(orc):
+    """Negative controls: the statistic rejects the wrong variant of each pinned choice -- the
+    in-sphere diffuse scatter (output/8.png, an earlier chapter variant), a pinhole for the
+    defocused chapter, and a solid glass sphere in the final scene."""
+    g = np.load(os.path.join(GOLDEN, "chapter_blocks.npz"))
+    on = _blocks(orc, CHAPTERS["c8_sampleOnSphere"], _chapter_camera(orc, "c8"), 1200, 600)
+    assert np.abs(on - g["c8"]).max() > 0.05   # 8.png: randomInUnitSphere scatter (measured 0.084)
+    pinhole = orc.camera_make((3, 3, 2), (0, 0, -1), 20.0, 2.0, 0.0, float(np.sqrt(27.0)))
+    assert np.abs(_blocks(orc, CHAPTERS["c11"], pinhole, 1200, 600) - g["c11"]).max() > 0.1
+    solid = [s for s in FINAL if s[1] != -0.9]
+    cam = orc.camera_make((13, 2, 3), (0, 0, 0), 20.0, 1.5, 0.1, 10.0)
+    assert np.abs(_blocks(orc, solid, cam, 1200, 800) - g["c13_mean"])[g["c13_consensus"]].max() > 0.1

@@ -7,6 +7,13 @@ exp2_blocks.npy — the reference's committed render output2/exp2.png (TRIANGLEW
   unbiased at any spp, which lets a low-spp oracle render be compared with it.  Rows are
   stored bottom-up (row 0 = bottom, the render kernel's order).
 
+chapter_blocks.npz — the reference's committed chapter renders output/{8_sampleOnSphere, 8, 9, 10,
+  11, 13, 13_1, 13_2}.png (the RTIOW chapter scenes the project was built through; their scene
+  code is no longer in the repository, tests/test_oracle.py restates them) as the same linear
+  block means.  13*.png are three renders of the final scene with different random small spheres:
+  stored as their mean and the mask of "consensus" blocks where the three agree within 0.004
+  (sky and the big spheres, untouched by the random spheres).
+
 usage: python tools/make_golden.py [/root/reference]
 """
 import os
@@ -82,6 +89,17 @@ def main() -> None:
     blocks = linear_blocks(img)
     np.save(os.path.join(out_dir, "exp2_blocks.npy"), blocks)
     print("exp2_blocks.npy", blocks.shape, float(blocks.mean()))
+    out = {}
+    for name in ("8_sampleOnSphere", "8", "9", "10", "11"):
+        img = read_png(os.path.join(ref, "output", name + ".png"))
+        assert img.shape[:2] == (600, 1200), (name, img.shape)
+        out["c" + name] = linear_blocks(img)
+    finals = [linear_blocks(read_png(os.path.join(ref, "output", n + ".png"))) for n in ("13", "13_1", "13_2")]
+    spread = np.max([np.abs(a - b) for a in finals for b in finals], axis=0).max(axis=2)
+    out["c13_mean"] = (sum(finals) / 3).astype(np.float32)
+    out["c13_consensus"] = spread < 0.004
+    np.savez_compressed(os.path.join(out_dir, "chapter_blocks.npz"), **out)
+    print("chapter_blocks.npz", {k: v.shape for k, v in out.items()}, int(out["c13_consensus"].sum()))
 
 
 if __name__ == "__main__":
