@@ -1047,6 +1047,25 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
+// Two rays per lane (sample mode, wide tree; PT_DUAL=1): each step swaps a lane's parked ray in
+// when only the parked one wants the step's kind, so more lanes work per step; 30 more VGPRs.
+#ifndef PT_DUAL
+#define PT_DUAL 0
+#endif
+#ifndef PT_DUAL_WAVES_PER_EU
+#define PT_DUAL_WAVES_PER_EU 4
+#endif
+template <bool SAMPLE, bool WIDE, bool INST>
+constexpr bool kDual = PT_DUAL != 0 && SAMPLE && WIDE && !INST;
+#ifdef PT_DUAL_ASM
+__device__ __forceinline__ void vswap(uint32_t& a, uint32_t& b) { asm volatile("v_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ void vswap(float& a, float& b) { asm volatile("v_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ void vswap(int& a, int& b) { asm volatile("v_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+#else
+template <class T>
+__device__ __forceinline__ void vswap(T& a, T& b) { const T t = a; a = b; b = t; }
+#endif
+__device__ __forceinline__ void vswap(float3& a, float3& b) { vswap(a.x, b.x); vswap(a.y, b.y); vswap(a.z, b.z); }
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kWavesPerEU = WIDE ? PT_WIDE_WAVES_PER_EU : kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
@@ -1093,23 +1112,27 @@ __device__ __forceinline__ DevScene ldScene(KArgs k) {
 // group would belong to another space), no reference-order redo (instanced frames are held to a
 // tolerance, not bit for bit).
 template <int STACK, bool SAMPLE, bool WIDE, bool INST = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAMPLE, WIDE, INST> ? PT_DUAL_WAVES_PER_EU : kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
     // Deep trees (binary kernels) keep 32 stack entries per lane in LDS (8 KB per wave: 5 waves
     // per SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
     constexpr int LS = kLdsStack<STACK, SAMPLE, WIDE>;
-    __shared__ uint32_t stk[LS * kWave];
+    // DUAL: two rays per lane (A in the step's registers, B parked in registers), each with its
+    // own LDS stack / parked group / task slot; a step swaps B in where only B wants the step's kind
+    constexpr bool DUAL = kDual<SAMPLE, WIDE, INST>;
+    constexpr int NR = DUAL ? 2 : 1;
+    __shared__ uint32_t stk[LS * kWave * NR];
     // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
     // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
     // marks it) and comes back when the current group is empty.
     constexpr int SPECN = (WIDE && !INST) ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
-    __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
+    __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave * NR : 1];
     // instanced scenes: the lane's world ray {o, d} while it is inside an instance
     __shared__ float wray[INST ? 6 * kWave : 1];
     // sample mode: the lane's task {pixel col | local row << 16, next sample, end sample, rays}.
     // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
     // in four VGPRs carried through every step.
-    __shared__ uint4 taskState[SAMPLE ? kWave : 1];
+    __shared__ uint4 taskState[SAMPLE ? kWave * NR : 1];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1132,13 +1155,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // gfx9 buffer resource: base = the node array, raw (stride 0), DATA_FORMAT_32 in dword 3
     const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(WIDE ? (const void*)S.wnodes : (const void*)S.nodes);
     uint32_t* my = stk + lane;
+    int tsl = lane, psl = lane;   // the current ray's task / parked-group slots (DUAL: its LDS half)
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
 #ifdef PT_DIAG
     uint32_t itN = 0, itL = 0, itS = 0, sPops = 0, sRedo = 0;   // scheduler diagnostics (iterations per kind)
     unsigned long long sSpecN = 0, sIdleN = 0;   // NODE steps: lanes waiting on primitives that have nodes left; lanes with no NODE work
-    unsigned long long cycN = 0, cycL = 0, cycS = 0;   // and shader cycles per kind
+    unsigned long long cycN = 0, cycL = 0, cycS = 0, cycH = 0;   // and shader cycles per kind, loop head
     unsigned long long cycSh = 0, cycTk = 0, cycNp = 0, cycBr = 0;   // SHADE: shading, tasks, new path, ray start
 #define PT_DIAG_ADD(v, x) (v) += (x)
 #else
@@ -1169,6 +1193,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     uint32_t depthPaths = 0;
     bool needTask = SAMPLE;
     uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode: the wave's reserved tasks (uniform)
+    // DUAL: the parked ray (B) and which LDS half the current ray (A) owns
+    float3 oB = o, dB = d, invB = inv, attB = att, sumB = sum;
+    float closestB = 0.0f, bestLoB = 0.0f;
+    int bestB = -1, depthLeftB = 0, spB = 0, sA = 0;
+    uint32_t ngB = 0u, tgB = 0u, tgBaseB = 0u, octB = 0u;
+    uint32_t gBd = 0u, gB0 = 0u, gB1 = 0u, gB2 = 0u, gB3 = 0u, gB4 = 0u;
+    bool activeB = false, needTaskB = DUAL;
 
 
     // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
@@ -1178,7 +1209,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         depthLeft--;                                                                              \
         if constexpr (SAMPLE) {   /* rays per task: only frames that measure tile costs use them */ \
             if (kargs()->measureCost)                                                             \
-                __hip_atomic_fetch_add(&taskState[lane].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+                __hip_atomic_fetch_add(&taskState[tsl].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
         }                                                                                         \
         closest = __builtin_inff();                                                               \
         best = -1;                                                                                \
@@ -1259,7 +1290,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                         needTask = false;                                                         \
                         got = true;                                                               \
                         const uint32_t s0_ = (hi_ ? blkB_ : blkA_) * (uint32_t)Q_.block;          \
-                        taskState[lane] = make_uint4((uint32_t)c_ | ((uint32_t)r_ << 16), s0_,     \
+                        taskState[tsl] = make_uint4((uint32_t)c_ | ((uint32_t)r_ << 16), s0_,     \
                                                      min(s0_ + (uint32_t)Q_.block, (uint32_t)Q_.spp), 0u); \
                         sum = f3(0.0f, 0.0f, 0.0f);                                               \
                     }                                                                             \
@@ -1281,7 +1312,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     do {                                                                                          \
         const auto& Q_ = *kargs();                                                                \
         if constexpr (SAMPLE) {   /* the task's pixel and next sample from LDS */                \
-            const uint4 ts_ = taskState[lane];                                                    \
+            const uint4 ts_ = taskState[tsl];                                                    \
             fcol = (float)(ts_.x & 0xffffu);                                                      \
             const uint32_t grow_ = (uint32_t)globalRowFast((int)(ts_.x >> 16), Q_.stripe_h, Q_.stripeShift, \
                                                            Q_.nparts, Q_.part);                  \
@@ -1309,10 +1340,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 PT_TAKE_TASKS(got);
                 if (__ballot(got) == 0) break;
                 if (got) {
-                    uint4 ts = taskState[lane];
+                    uint4 ts = taskState[tsl];
                     depthPaths += ts.z - ts.y;
                     for (; ts.y < ts.z; ts.y++) {
-                        taskState[lane].y = ts.y;
+                        taskState[tsl].y = ts.y;
                         PT_NEW_PATH();
                         sum = add(sum, sky(d, att));
                     }
@@ -1340,16 +1371,27 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
               (!SAMPLE && P.max_depth <= 0 ? (uint32_t)__popcll(__ballot(valid)) * (uint32_t)nSamples : 0u);
 
     for (;;) {
+#ifdef PT_DIAG
+        const unsigned long long tH0 = __builtin_amdgcn_s_memtime();
+#endif
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
-        const bool wantNode = WIDE ? ((SPEC ? (tg == 0u || ((oct >> 4) & 3u) < (uint32_t)SPECN) : tg == 0u) &&
-                                      ((ng & 0xffu) != 0u || sp > 0))
-                                   : (node >= 0 && qn <= LQ - 2);
-        const bool wantLeaf = WIDE ? tg != 0u : qn > 0;
-        const bool wantShade = (active && (WIDE ? (tg == 0u && (ng & 0xffu) == 0u && sp == 0) : (node == -1 && qn == 0))) ||
-                               needTask;
-        const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
+#define PT_WANT_NODE(ng_, tg_, sp_, oct_) \
+        (WIDE ? ((SPEC ? ((tg_) == 0u || (((oct_) >> 4) & 3u) < (uint32_t)SPECN) : (tg_) == 0u) && (((ng_) & 0xffu) != 0u || (sp_) > 0)) \
+              : (node >= 0 && qn <= LQ - 2))
+#define PT_WANT_SHADE(ng_, tg_, sp_, active_, needTask_) \
+        (((active_) && (WIDE ? ((tg_) == 0u && ((ng_) & 0xffu) == 0u && (sp_) == 0) : (node == -1 && qn == 0))) || (needTask_))
+        bool wantNode = PT_WANT_NODE(ng, tg, sp, oct);
+        bool wantLeaf = WIDE ? tg != 0u : qn > 0;
+        bool wantShade = PT_WANT_SHADE(ng, tg, sp, active, needTask);
+        bool bN = false, bL = false, bS = false;   // DUAL: what the parked ray wants
+        if constexpr (DUAL) {
+            bN = PT_WANT_NODE(ngB, tgB, spB, octB);
+            bL = tgB != 0u;
+            bS = PT_WANT_SHADE(ngB, tgB, spB, activeB, needTaskB);
+        }
+        const uint64_t mN = __ballot(wantNode || bN), mL = __ballot(wantLeaf || bL), mS = __ballot(wantShade || bS);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
         int kind;   // 0 node, 1 leaf, 2 shade
@@ -1358,8 +1400,36 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         else if (nS >= P.shadeBatch) kind = 2;
         else if (!SAMPLE && nN < P.nodeMin && (nL | nS)) kind = nL >= nS ? 1 : 2;
         else kind = 0;
+        if constexpr (DUAL) {   // lanes whose parked ray alone wants this kind swap it in
+            const bool useB = kind == 0 ? (!wantNode && bN) : (kind == 1 ? (!wantLeaf && bL) : (!wantShade && bS));
+            if (__ballot(useB)) {
+                if (useB) {
+                    vswap(o, oB); vswap(d, dB); vswap(inv, invB); vswap(att, attB); vswap(sum, sumB);
+                    vswap(closest, closestB); vswap(bestLo, bestLoB); vswap(best, bestB);
+                    vswap(depthLeft, depthLeftB); vswap(sp, spB);
+                    vswap(ng, ngB); vswap(tg, tgB); vswap(tgBase, tgBaseB); vswap(oct, octB);
+                    vswap(g.d, gBd); vswap(g.v0, gB0); vswap(g.v1, gB1); vswap(g.v2, gB2); vswap(g.v3, gB3);
+                    vswap(g.v4, gB4);
+                    sA ^= 1;
+                }
+                const bool ta = active, tn = needTask;
+                active = useB ? activeB : active;
+                activeB = useB ? ta : activeB;
+                needTask = useB ? needTaskB : needTask;
+                needTaskB = useB ? tn : needTaskB;
+                my = stk + lane + sA * (LS * kWave);
+                tsl = lane + sA * kWave;
+                psl = lane + sA * (2 * SPECN * kWave);
+                wantNode = PT_WANT_NODE(ng, tg, sp, oct);
+                wantLeaf = tg != 0u;
+                wantShade = PT_WANT_SHADE(ng, tg, sp, active, needTask);
+            }
+        }
+#undef PT_WANT_NODE
+#undef PT_WANT_SHADE
 #ifdef PT_DIAG
         const unsigned long long tK0 = __builtin_amdgcn_s_memtime();
+        cycH += tK0 - tH0;
 #endif
 
         if (kind == 0) {
@@ -1423,8 +1493,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (wantNode) {
                     if (SPEC && tg != 0u) {   // park the waiting primitive group, keep traversing
                         const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
-                        pend[(2u * c) * kWave + lane] = tgBase;
-                        pend[(2u * c + 1u) * kWave + lane] = tg;
+                        pend[(2u * c) * kWave + psl] = tgBase;
+                        pend[(2u * c + 1u) * kWave + psl] = tg;
                         oct += 16u;
                     }
                     // (the parked values are read back from LDS, not kept in registers meanwhile)
@@ -1447,8 +1517,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     if (SPEC && tg == 0u && (oct & 48u)) {   // no new primitives: the last parked group is current again
                         oct -= 16u;
                         const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
-                        tgBase = pend[(2u * c) * kWave + lane];
-                        tg = pend[(2u * c + 1u) * kWave + lane];
+                        tgBase = pend[(2u * c) * kWave + psl];
+                        tg = pend[(2u * c + 1u) * kWave + psl];
                     }
                 }
             } else if (wantNode) {
@@ -1551,8 +1621,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (SPEC && tg == 0u && (oct & 48u)) {   // this group is done: the last parked one is next
                     oct -= 16u;
                     const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
-                    tgBase = pend[(2u * c) * kWave + lane];
-                    tg = pend[(2u * c + 1u) * kWave + lane];
+                    tgBase = pend[(2u * c) * kWave + psl];
+                    tg = pend[(2u * c + 1u) * kWave + psl];
                 }
             } else {
             // Every lane tests all of its queued leaves, in order, in this step (the queue then
@@ -1631,9 +1701,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (done) {
                     sum = add(sum, contrib);
                     if constexpr (SAMPLE) {
-                        uint4 ts = taskState[lane];
+                        uint4 ts = taskState[tsl];
                         ts.y++;
-                        taskState[lane].y = ts.y;
+                        taskState[tsl].y = ts.y;
                         if (ts.y == ts.z) {
                             active = false;
                             PT_FINISH_TASK(ts);
@@ -1717,6 +1787,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         atomicAdd(P.counters + 12, cycN);
         atomicAdd(P.counters + 13, cycL);
         atomicAdd(P.counters + 14, cycS);
+        atomicAdd(P.counters + 15, cycH);
         atomicAdd(P.counters + 16, cycSh);
         atomicAdd(P.counters + 17, cycTk);
         atomicAdd(P.counters + 18, cycNp);
@@ -2899,6 +2970,9 @@ void printIterStats(const unsigned long long* c, bool wide) {
         std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps); NODE steps: "
                      "lanes waiting on primitives with nodes left %.1f, lanes without NODE work %.1f\n", c[20],
                      (double)c[21] / std::max(1ull, c[8]), (double)c[22] / std::max(1ull, c[8]));
+    if (c[15] > 0)
+        std::fprintf(stderr, "[pt] loop head (choice of the step kind) cycles/iteration %.0f\n",
+                     (double)c[15] / std::max(1ull, c[8] + c[9] + c[10]));
     if (c[14] > 0)
         std::fprintf(stderr, "[pt] SHADE cycles/iteration: shading %.0f tasks %.0f new-path %.0f ray-start %.0f\n",
                      (double)c[16] / std::max(1ull, c[10]), (double)c[17] / std::max(1ull, c[10]),
@@ -3549,6 +3623,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if ((rc = persistentWavesPerCU(stack, kernel, perCU, s->instanced))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
+        if (std::getenv("PT_ITER_STATS"))
+            std::fprintf(stderr, "[pt] persistent waves %d (%d per CU, stack %d)\n", P.nwaves, perCU, stack);
         // Tile costs (rays of the tile's most expensive pixel) are measured on the first frame and
         // then on one frame in eight: the order only steers the launch's tail, and counting costs
         // one more atomic per task.
