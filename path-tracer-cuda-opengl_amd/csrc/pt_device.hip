@@ -1047,25 +1047,6 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
-// Two rays per lane (sample mode, wide tree; PT_DUAL=1): each step swaps a lane's parked ray in
-// when only the parked one wants the step's kind, so more lanes work per step; 30 more VGPRs.
-#ifndef PT_DUAL
-#define PT_DUAL 0
-#endif
-#ifndef PT_DUAL_WAVES_PER_EU
-#define PT_DUAL_WAVES_PER_EU 4
-#endif
-template <bool SAMPLE, bool WIDE, bool INST>
-constexpr bool kDual = PT_DUAL != 0 && SAMPLE && WIDE && !INST;
-#ifdef PT_DUAL_ASM
-__device__ __forceinline__ void vswap(uint32_t& a, uint32_t& b) { asm volatile("v_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
-__device__ __forceinline__ void vswap(float& a, float& b) { asm volatile("v_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
-__device__ __forceinline__ void vswap(int& a, int& b) { asm volatile("v_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
-#else
-template <class T>
-__device__ __forceinline__ void vswap(T& a, T& b) { const T t = a; a = b; b = t; }
-#endif
-__device__ __forceinline__ void vswap(float3& a, float3& b) { vswap(a.x, b.x); vswap(a.y, b.y); vswap(a.z, b.z); }
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kWavesPerEU = WIDE ? PT_WIDE_WAVES_PER_EU : kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
@@ -1112,27 +1093,23 @@ __device__ __forceinline__ DevScene ldScene(KArgs k) {
 // group would belong to another space), no reference-order redo (instanced frames are held to a
 // tolerance, not bit for bit).
 template <int STACK, bool SAMPLE, bool WIDE, bool INST = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAMPLE, WIDE, INST> ? PT_DUAL_WAVES_PER_EU : kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<STACK, SAMPLE, WIDE>))) void renderKernelWF(RenderParams P) {
     // Deep trees (binary kernels) keep 32 stack entries per lane in LDS (8 KB per wave: 5 waves
     // per SIMD) and the rare deeper entries in global memory (stackSpill, per wave slot and lane).
     constexpr int LS = kLdsStack<STACK, SAMPLE, WIDE>;
-    // DUAL: two rays per lane (A in the step's registers, B parked in registers), each with its
-    // own LDS stack / parked group / task slot; a step swaps B in where only B wants the step's kind
-    constexpr bool DUAL = kDual<SAMPLE, WIDE, INST>;
-    constexpr int NR = DUAL ? 2 : 1;
-    __shared__ uint32_t stk[LS * kWave * NR];
+    __shared__ uint32_t stk[LS * kWave];
     // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
     // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
     // marks it) and comes back when the current group is empty.
     constexpr int SPECN = (WIDE && !INST) ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
-    __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave * NR : 1];
+    __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
     // instanced scenes: the lane's world ray {o, d} while it is inside an instance
     __shared__ float wray[INST ? 6 * kWave : 1];
     // sample mode: the lane's task {pixel col | local row << 16, next sample, end sample, rays}.
     // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
     // in four VGPRs carried through every step.
-    __shared__ uint4 taskState[SAMPLE ? kWave * NR : 1];
+    __shared__ uint4 taskState[SAMPLE ? kWave : 1];
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1155,7 +1132,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
     // gfx9 buffer resource: base = the node array, raw (stride 0), DATA_FORMAT_32 in dword 3
     const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(WIDE ? (const void*)S.wnodes : (const void*)S.nodes);
     uint32_t* my = stk + lane;
-    int tsl = lane, psl = lane;   // the current ray's task / parked-group slots (DUAL: its LDS half)
     // Work counters are wave totals kept in scalar registers: each step adds the popcount of
     // a ballot of the lanes that did the work (no per-lane counter VGPRs).
     uint32_t sRays = 0, sVisits = 0, sTris = 0, sSph = 0, sPaths = 0;
@@ -1193,13 +1169,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
     uint32_t depthPaths = 0;
     bool needTask = SAMPLE;
     uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode: the wave's reserved tasks (uniform)
-    // DUAL: the parked ray (B) and which LDS half the current ray (A) owns
-    float3 oB = o, dB = d, invB = inv, attB = att, sumB = sum;
-    float closestB = 0.0f, bestLoB = 0.0f;
-    int bestB = -1, depthLeftB = 0, spB = 0, sA = 0;
-    uint32_t ngB = 0u, tgB = 0u, tgBaseB = 0u, octB = 0u;
-    uint32_t gBd = 0u, gB0 = 0u, gB1 = 0u, gB2 = 0u, gB3 = 0u, gB4 = 0u;
-    bool activeB = false, needTaskB = DUAL;
 
 
     // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
@@ -1209,7 +1178,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
         depthLeft--;                                                                              \
         if constexpr (SAMPLE) {   /* rays per task: only frames that measure tile costs use them */ \
             if (kargs()->measureCost)                                                             \
-                __hip_atomic_fetch_add(&taskState[tsl].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+                __hip_atomic_fetch_add(&taskState[lane].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
         }                                                                                         \
         closest = __builtin_inff();                                                               \
         best = -1;                                                                                \
@@ -1290,7 +1259,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
                         needTask = false;                                                         \
                         got = true;                                                               \
                         const uint32_t s0_ = (hi_ ? blkB_ : blkA_) * (uint32_t)Q_.block;          \
-                        taskState[tsl] = make_uint4((uint32_t)c_ | ((uint32_t)r_ << 16), s0_,     \
+                        taskState[lane] = make_uint4((uint32_t)c_ | ((uint32_t)r_ << 16), s0_,     \
                                                      min(s0_ + (uint32_t)Q_.block, (uint32_t)Q_.spp), 0u); \
                         sum = f3(0.0f, 0.0f, 0.0f);                                               \
                     }                                                                             \
@@ -1312,7 +1281,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
     do {                                                                                          \
         const auto& Q_ = *kargs();                                                                \
         if constexpr (SAMPLE) {   /* the task's pixel and next sample from LDS */                \
-            const uint4 ts_ = taskState[tsl];                                                    \
+            const uint4 ts_ = taskState[lane];                                                    \
             fcol = (float)(ts_.x & 0xffffu);                                                      \
             const uint32_t grow_ = (uint32_t)globalRowFast((int)(ts_.x >> 16), Q_.stripe_h, Q_.stripeShift, \
                                                            Q_.nparts, Q_.part);                  \
@@ -1340,10 +1309,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
                 PT_TAKE_TASKS(got);
                 if (__ballot(got) == 0) break;
                 if (got) {
-                    uint4 ts = taskState[tsl];
+                    uint4 ts = taskState[lane];
                     depthPaths += ts.z - ts.y;
                     for (; ts.y < ts.z; ts.y++) {
-                        taskState[tsl].y = ts.y;
+                        taskState[lane].y = ts.y;
                         PT_NEW_PATH();
                         sum = add(sum, sky(d, att));
                     }
@@ -1377,21 +1346,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
-#define PT_WANT_NODE(ng_, tg_, sp_, oct_) \
-        (WIDE ? ((SPEC ? ((tg_) == 0u || (((oct_) >> 4) & 3u) < (uint32_t)SPECN) : (tg_) == 0u) && (((ng_) & 0xffu) != 0u || (sp_) > 0)) \
-              : (node >= 0 && qn <= LQ - 2))
-#define PT_WANT_SHADE(ng_, tg_, sp_, active_, needTask_) \
-        (((active_) && (WIDE ? ((tg_) == 0u && ((ng_) & 0xffu) == 0u && (sp_) == 0) : (node == -1 && qn == 0))) || (needTask_))
-        bool wantNode = PT_WANT_NODE(ng, tg, sp, oct);
-        bool wantLeaf = WIDE ? tg != 0u : qn > 0;
-        bool wantShade = PT_WANT_SHADE(ng, tg, sp, active, needTask);
-        bool bN = false, bL = false, bS = false;   // DUAL: what the parked ray wants
-        if constexpr (DUAL) {
-            bN = PT_WANT_NODE(ngB, tgB, spB, octB);
-            bL = tgB != 0u;
-            bS = PT_WANT_SHADE(ngB, tgB, spB, activeB, needTaskB);
-        }
-        const uint64_t mN = __ballot(wantNode || bN), mL = __ballot(wantLeaf || bL), mS = __ballot(wantShade || bS);
+        const bool wantNode = WIDE ? ((SPEC ? (tg == 0u || ((oct >> 4) & 3u) < (uint32_t)SPECN) : tg == 0u) &&
+                                      ((ng & 0xffu) != 0u || sp > 0))
+                                   : (node >= 0 && qn <= LQ - 2);
+        const bool wantLeaf = WIDE ? tg != 0u : qn > 0;
+        const bool wantShade = (active && (WIDE ? (tg == 0u && (ng & 0xffu) == 0u && sp == 0) : (node == -1 && qn == 0))) ||
+                               needTask;
+        const uint64_t mN = __ballot(wantNode), mL = __ballot(wantLeaf), mS = __ballot(wantShade);
         if ((mN | mL | mS) == 0) break;
         const int nN = __popcll(mN), nL = __popcll(mL), nS = __popcll(mS);
         int kind;   // 0 node, 1 leaf, 2 shade
@@ -1400,33 +1361,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
         else if (nS >= P.shadeBatch) kind = 2;
         else if (!SAMPLE && nN < P.nodeMin && (nL | nS)) kind = nL >= nS ? 1 : 2;
         else kind = 0;
-        if constexpr (DUAL) {   // lanes whose parked ray alone wants this kind swap it in
-            const bool useB = kind == 0 ? (!wantNode && bN) : (kind == 1 ? (!wantLeaf && bL) : (!wantShade && bS));
-            if (__ballot(useB)) {
-                if (useB) {
-                    vswap(o, oB); vswap(d, dB); vswap(inv, invB); vswap(att, attB); vswap(sum, sumB);
-                    vswap(closest, closestB); vswap(bestLo, bestLoB); vswap(best, bestB);
-                    vswap(depthLeft, depthLeftB); vswap(sp, spB);
-                    vswap(ng, ngB); vswap(tg, tgB); vswap(tgBase, tgBaseB); vswap(oct, octB);
-                    vswap(g.d, gBd); vswap(g.v0, gB0); vswap(g.v1, gB1); vswap(g.v2, gB2); vswap(g.v3, gB3);
-                    vswap(g.v4, gB4);
-                    sA ^= 1;
-                }
-                const bool ta = active, tn = needTask;
-                active = useB ? activeB : active;
-                activeB = useB ? ta : activeB;
-                needTask = useB ? needTaskB : needTask;
-                needTaskB = useB ? tn : needTaskB;
-                my = stk + lane + sA * (LS * kWave);
-                tsl = lane + sA * kWave;
-                psl = lane + sA * (2 * SPECN * kWave);
-                wantNode = PT_WANT_NODE(ng, tg, sp, oct);
-                wantLeaf = tg != 0u;
-                wantShade = PT_WANT_SHADE(ng, tg, sp, active, needTask);
-            }
-        }
-#undef PT_WANT_NODE
-#undef PT_WANT_SHADE
 #ifdef PT_DIAG
         const unsigned long long tK0 = __builtin_amdgcn_s_memtime();
         cycH += tK0 - tH0;
@@ -1493,8 +1427,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
                 if (wantNode) {
                     if (SPEC && tg != 0u) {   // park the waiting primitive group, keep traversing
                         const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
-                        pend[(2u * c) * kWave + psl] = tgBase;
-                        pend[(2u * c + 1u) * kWave + psl] = tg;
+                        pend[(2u * c) * kWave + lane] = tgBase;
+                        pend[(2u * c + 1u) * kWave + lane] = tg;
                         oct += 16u;
                     }
                     // (the parked values are read back from LDS, not kept in registers meanwhile)
@@ -1517,8 +1451,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
                     if (SPEC && tg == 0u && (oct & 48u)) {   // no new primitives: the last parked group is current again
                         oct -= 16u;
                         const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
-                        tgBase = pend[(2u * c) * kWave + psl];
-                        tg = pend[(2u * c + 1u) * kWave + psl];
+                        tgBase = pend[(2u * c) * kWave + lane];
+                        tg = pend[(2u * c + 1u) * kWave + lane];
                     }
                 }
             } else if (wantNode) {
@@ -1621,8 +1555,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
                 if (SPEC && tg == 0u && (oct & 48u)) {   // this group is done: the last parked one is next
                     oct -= 16u;
                     const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
-                    tgBase = pend[(2u * c) * kWave + psl];
-                    tg = pend[(2u * c + 1u) * kWave + psl];
+                    tgBase = pend[(2u * c) * kWave + lane];
+                    tg = pend[(2u * c + 1u) * kWave + lane];
                 }
             } else {
             // Every lane tests all of its queued leaves, in order, in this step (the queue then
@@ -1701,9 +1635,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kDual<SAM
                 if (done) {
                     sum = add(sum, contrib);
                     if constexpr (SAMPLE) {
-                        uint4 ts = taskState[tsl];
+                        uint4 ts = taskState[lane];
                         ts.y++;
-                        taskState[tsl].y = ts.y;
+                        taskState[lane].y = ts.y;
                         if (ts.y == ts.z) {
                             active = false;
                             PT_FINISH_TASK(ts);
