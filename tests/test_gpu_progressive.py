@@ -200,6 +200,36 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     np.testing.assert_array_equal(read_png(one), read_png(two))
 
 
+def test_bench_c4_eight_ranks_rehearsal(tmp_path):
+    """C4 (BASELINE.json configs[3]: the C3 scene at 1920x1080, 4096 spp, row-tiled over 8 GPUs)
+    through bench.py's own multi-rank flow: 8 ranks over gloo sharing this one GPU (a rehearsal,
+    never a reported number), each rendering its 1/8 of the stripes at the full sample count; the
+    gathered, un-permuted PNG equals the 1-rank PNG byte for byte and the rank-0 line reports the
+    whole frame's rays."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from helpers import read_png
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--config", "c4", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-compat",
+              "--no-interactive"]
+    one, eight = str(tmp_path / "one.png"), str(tmp_path / "eight.png")
+    r1 = subprocess.run([sys.executable] + common + ["--png", one], cwd=repo, capture_output=True, text=True,
+                        timeout=600)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    env = dict(os.environ, PT_DIST_BACKEND="gloo")
+    r8 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                         "--master-addr", "127.0.0.1", "--master-port", "29518"] + common[:1] + ["--gpus", "8"] +
+                        common[1:] + ["--png", eight], cwd=repo, capture_output=True, text=True, timeout=600, env=env)
+    assert r8.returncode == 0, r8.stderr[-2000:]
+    np.testing.assert_array_equal(read_png(one), read_png(eight))
+    l1 = json.loads([x for x in r1.stdout.splitlines() if x.startswith("{")][-1])
+    l8 = json.loads([x for x in r8.stdout.splitlines() if x.startswith("{")][-1])
+    assert l1["config"]["spp"] == l8["config"]["spp"] == 4096 and l8["n_gpus"] == 8
+    assert l1["config"]["rays_per_frame"] == l8["config"]["rays_per_frame"] > 4 * 1920 * 1080 * 4096
+
+
 @pytest.mark.parametrize("rng", ["compat", "sample"])
 def test_async_frames_match_synchronous(pt, setup, rng):
     """pt_render_ex with a device output and no pt_stats returns before the frame is done
