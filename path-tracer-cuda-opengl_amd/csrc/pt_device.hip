@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -76,6 +77,7 @@ struct DevScene {
     int nprims;
     int hasSpheres;          // 0: triangles only (the wide kernels' LEAF tests drop the sphere tie rules)
     float cx, cy, cz, ext;   // tight scene box: centre and largest extent (the wide kernels' far-origin test)
+    float mixLim;            // largest finite |1 / d| component the MIX plane arithmetic takes (wideHits, mixUnsafe)
     // instanced scenes (renderKernelWF<.., INST>): per instance {world-to-object rows r0, r1, r2}
     // {objBase, identity, 0, 0}; a hit's key is instance << gBits | its primitive's shading index
     const float4* winst;
@@ -417,11 +419,18 @@ __device__ __forceinline__ void wideTest(const Prim& q, float3 o, float3 d, floa
 // and its coordinates (the quantum is >= 2^-18 of that, the rounding of the ray's plane distances
 // about 2^-21.6 of |p - o|): a ray whose origin lies farther than 8 scene extents from the
 // scene's centre (wideFar) skips this test and is traced in the reference's order instead.
+//
+// MIX: the plane bytes as fp16 denormals into v_fma_mix_f32 (pt_math.hpp fmaMixLo), the scales
+// a = s * inv taken times 2^24 -- the same t bit for bit while |s * 2^24 * inv| stays finite,
+// which holds for |inv| <= DevScene::mixLim (a ray with a larger finite |inv| component takes the
+// reference-order query instead: mixUnsafe).
+template <bool MIX = false>
 __device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4 n3, uint4 n4, float3 o, float3 inv,
                                              uint32_t oct, float tmin, float tmax) {
-    const float ax = __uint_as_float((n0.w & 0xffu) << 23) * inv.x;
-    const float ay = __uint_as_float(((n0.w >> 8) & 0xffu) << 23) * inv.y;
-    const float az = __uint_as_float(((n0.w >> 16) & 0xffu) << 23) * inv.z;
+    constexpr uint32_t kMixExp = MIX ? 24u : 0u;   // s * 2^24: the exponent byte + 24 (< 255: mixLim's bound)
+    const float ax = __uint_as_float(((n0.w & 0xffu) + kMixExp) << 23) * inv.x;
+    const float ay = __uint_as_float((((n0.w >> 8) & 0xffu) + kMixExp) << 23) * inv.y;
+    const float az = __uint_as_float((((n0.w >> 16) & 0xffu) + kMixExp) << 23) * inv.z;
     const float bx = (__uint_as_float(n0.x) - o.x) * inv.x;
     const float by = (__uint_as_float(n0.y) - o.y) * inv.y;
     const float bz = (__uint_as_float(n0.z) - o.z) * inv.z;
@@ -446,14 +455,39 @@ __device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4
         const uint32_t childBits4 = (meta4 >> 5) & 0x07070707u;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const float tnx = __builtin_fmaf((float)((nearX[h] >> (8 * j)) & 0xffu), ax, bx);
-            const float tny = __builtin_fmaf((float)((nearY[h] >> (8 * j)) & 0xffu), ay, by);
-            const float tnz = __builtin_fmaf((float)((nearZ[h] >> (8 * j)) & 0xffu), az, bz);
-            const float tfx = __builtin_fmaf((float)((farX[h] >> (8 * j)) & 0xffu), ax, bx);
-            const float tfy = __builtin_fmaf((float)((farY[h] >> (8 * j)) & 0xffu), ay, by);
-            const float tfz = __builtin_fmaf((float)((farZ[h] >> (8 * j)) & 0xffu), az, bz);
-            const float lo = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), tmin);
-            const float hi = fminf(fminf(fminf(tfx, tfy), tfz), tmax);
+            float tnx, tny, tnz, tfx, tfy, tfz;
+            if constexpr (MIX) {   // children j, j ^ 1 share an fp16 pair (the perms are redone per child:
+                                   // cheaper in registers than six pairs live across two children)
+                const bool hi = (j & 2) != 0;
+                const uint32_t px = hi ? planePairHi(nearX[h]) : planePairLo(nearX[h]);
+                const uint32_t py = hi ? planePairHi(nearY[h]) : planePairLo(nearY[h]);
+                const uint32_t pz = hi ? planePairHi(nearZ[h]) : planePairLo(nearZ[h]);
+                const uint32_t qx = hi ? planePairHi(farX[h]) : planePairLo(farX[h]);
+                const uint32_t qy = hi ? planePairHi(farY[h]) : planePairLo(farY[h]);
+                const uint32_t qz = hi ? planePairHi(farZ[h]) : planePairLo(farZ[h]);
+                if (j & 1) {
+                    tnx = fmaMixHi(px, ax, bx); tny = fmaMixHi(py, ay, by); tnz = fmaMixHi(pz, az, bz);
+                    tfx = fmaMixHi(qx, ax, bx); tfy = fmaMixHi(qy, ay, by); tfz = fmaMixHi(qz, az, bz);
+                } else {
+                    tnx = fmaMixLo(px, ax, bx); tny = fmaMixLo(py, ay, by); tnz = fmaMixLo(pz, az, bz);
+                    tfx = fmaMixLo(qx, ax, bx); tfy = fmaMixLo(qy, ay, by); tfz = fmaMixLo(qz, az, bz);
+                }
+            } else {
+                tnx = __builtin_fmaf((float)((nearX[h] >> (8 * j)) & 0xffu), ax, bx);
+                tny = __builtin_fmaf((float)((nearY[h] >> (8 * j)) & 0xffu), ay, by);
+                tnz = __builtin_fmaf((float)((nearZ[h] >> (8 * j)) & 0xffu), az, bz);
+                tfx = __builtin_fmaf((float)((farX[h] >> (8 * j)) & 0xffu), ax, bx);
+                tfy = __builtin_fmaf((float)((farY[h] >> (8 * j)) & 0xffu), ay, by);
+                tfz = __builtin_fmaf((float)((farZ[h] >> (8 * j)) & 0xffu), az, bz);
+            }
+            float lo, hi;
+            if (MIX && (j & 1)) {
+                lo = max3Raw(max3Raw(tnx, tny, tnz), tmin, tmin);
+                hi = min3Raw(min3Raw(tfx, tfy, tfz), tmax, tmax);
+            } else {
+                lo = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), tmin);
+                hi = fminf(fminf(fminf(tfx, tfy), tfz), tmax);
+            }
             const uint32_t bits = ((childBits4 >> (8 * j)) & 0xffu) << ((bitIndex4 >> (8 * j)) & 0xffu);
             hits |= lo <= hi ? bits : 0u;
         }
@@ -468,6 +502,16 @@ __device__ __forceinline__ bool wideFar(float cx, float cy, float cz, float ext,
     return !(m <= 8.0f * ext);   // (NaN: far)
 }
 __device__ __forceinline__ bool wideFar(const DevScene& S, float3 o) { return wideFar(S.cx, S.cy, S.cz, S.ext, o); }
+
+// A reciprocal direction component that is finite but larger than `lim` (DevScene::mixLim: a ray
+// nearly parallel to an axis plane) would overflow the MIX plane scale s * 2^24 * inv (wideHits);
+// such a ray takes the reference-order query.  (An infinite component is fine: both forms then
+// compute the same infinities and NaNs.  NaN: unsafe.)
+__device__ __forceinline__ bool mixUnsafe(float3 inv, float lim) {
+    const float x = fabsf(inv.x), y = fabsf(inv.y), z = fabsf(inv.z);
+    return (!(x <= lim) && x != __builtin_inff()) || (!(y <= lim) && y != __builtin_inff()) ||
+           (!(z <= lim) && z != __builtin_inff());
+}
 
 // RenderManager::hitBvh (render_manager.h:86-135): same visiting order (left child, right
 // child, leaf children tested at once, internal children pushed left then right).
@@ -1044,6 +1088,12 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #ifndef PT_WIDE_SPEC
 #define PT_WIDE_SPEC 1   // wide kernels: speculative traversal, primitive groups a lane may park while it keeps visiting nodes (0-3)
 #endif
+#ifndef PT_WIDE_MIX
+#define PT_WIDE_MIX 1   // wide kernels: plane distances by v_perm + v_fma_mix_f32 (wideHits<MIX>), bit-identical
+#endif
+#ifndef PT_MIX_CHECK
+#define PT_MIX_CHECK 1   // (A/B timing only: 0 drops the per-ray mixUnsafe test -- not exact for near-axis rays)
+#endif
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
@@ -1083,6 +1133,7 @@ __device__ __forceinline__ DevScene ldScene(KArgs k) {
     S.iparent = k->S.iparent; S.err = k->S.err; S.nprims = k->S.nprims;
     S.hasSpheres = k->S.hasSpheres;
     S.cx = k->S.cx; S.cy = k->S.cy; S.cz = k->S.cz; S.ext = k->S.ext;
+    S.mixLim = k->S.mixLim;
     S.winst = k->S.winst; S.gBits = k->S.gBits;
     return S;
 }
@@ -1193,9 +1244,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             ng = S.nprims > 0 ? (1u << oc_) : 0u;                                                 \
             /* only camera rays can start far from the scene (a bounce starts on a primitive), and  \
                they all start at the camera: one uniform flag, set on the host (wideFar) */     \
-            if (!INST && kargs()->camFar && depthLeft + 1 == kargs()->max_depth) {                 \
-                ng = 0u;       /* origin far from the scene: no wide traversal, */                 \
-                oct |= 8u;     /* the query in the reference's order (SHADE's redo) */             \
+            if (!INST && ((kargs()->camFar && depthLeft + 1 == kargs()->max_depth) ||              \
+                          (PT_WIDE_MIX && PT_MIX_CHECK && mixUnsafe(inv, kargs()->S.mixLim)))) {                  \
+                ng = 0u;       /* origin far from the scene, or a direction the MIX planes */      \
+                oct |= 8u;     /* cannot take: the query in the reference's order (SHADE's redo) */ \
             }                                                                                     \
         } else if (S.nprims <= 1) {                                                               \
             node = -1;                                                                            \
@@ -1444,7 +1496,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
                     const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
                     const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
-                    const uint32_t hits = wideHits(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
+                    const uint32_t hits = wideHits<PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
                     ng = (n1.x << 8) | (hits >> 24);
                     tgBase = n1.y;
                     tg = hits & 0xffffffu;
@@ -1867,7 +1919,8 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
         const uint32_t woct = (winv.x < 0.0f ? 1u : 0u) | (winv.y < 0.0f ? 2u : 0u) | (winv.z < 0.0f ? 4u : 0u);
         float3 o = wo, d = wd, inv = winv;   // (inside an instance: its object space)
         uint32_t oct = woct, inst = 0u;
-        const bool far = !INST && wideFar(S, o);   // (then: the query in the reference's order only)
+        // (far origin, or a direction the MIX planes cannot take: the query in the reference's order only)
+        const bool far = !INST && (wideFar(S, o) || (PT_WIDE_MIX && mixUnsafe(winv, S.mixLim)));
         float closest = tmax;
         int best = -1, sp = 0;
         bool redo = far;
@@ -1931,7 +1984,7 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 tg = 0u;
                 continue;
             }
-            const uint32_t h = wideHits(n0, n1, n2, n3, n4, o, inv, oct, tmin, closest);
+            const uint32_t h = wideHits<!INST && PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tmin, closest);
             ng = (n1.x << 8) | (h >> 24);
             tgBase = n1.y;
             tg = h & 0xffffffu;
@@ -2396,6 +2449,7 @@ struct pt_scene {
     size_t deviceBytes = 0;
     double buildMs = 0.0;                   // last pt_scene_build_bvh, device time (HIP events)
     float sceneCE[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // tight scene box: centre, largest extent (DevScene)
+    float mixLim = -1.0f;                          // DevScene::mixLim (-1: every ray takes the reference order)
     // instanced scenes (pt_scene_create_instanced): meshes = object ranges of `objs`, instances
     bool instanced = false;
     std::vector<int64_t> meshFirst, meshCount;
@@ -2853,6 +2907,21 @@ int filmInit(pt_film* f, hipStream_t st) {
     return PT_OK;
 }
 
+// DevScene::mixLim for a scene whose coordinates and extent are at most m.  Both wide builders
+// (host/pt_wide8.cpp, csrc/pt_wide_build.hip) give a node the plane quantum s = 2^e with e the
+// larger of ceil(log2(m)) - 18 and ceil(log2(node extent / 251)), so s <= 2^eS with
+// eS = ceil(log2(m)) + 1; then |s * 2^24 * inv| < 2^128 (finite) for |inv| <= 2^(103 - eS), and the
+// exponent byte + 24 stays below 255 for eS <= 100.  Beyond that, every ray takes the reference order.
+float mixLimit(double m) {
+    if (!(m > 0.0) || !std::isfinite(m)) return m == 0.0 ? FLT_MAX : -1.0f;
+    int ex = 0;
+    const double f = std::frexp(m, &ex);   // m = f * 2^ex, f in [0.5, 1): ceil(log2(m)) = ex, or ex - 1 at f = 0.5
+    const int eS = (f == 0.5 ? ex - 1 : ex) + 1;
+    if (eS > 100) return -1.0f;
+    if (103 - eS >= 127) return FLT_MAX;
+    return std::ldexp(1.0f, 103 - eS);
+}
+
 DevScene devScene(const pt_scene* s) {
     DevScene S;
     S.nodes = s->nodes.as<float4>();
@@ -2868,6 +2937,7 @@ DevScene devScene(const pt_scene* s) {
     S.nprims = (int)s->nobj;
     S.hasSpheres = s->hasSpheres ? 1 : 0;
     S.cx = s->sceneCE[0]; S.cy = s->sceneCE[1]; S.cz = s->sceneCE[2]; S.ext = s->sceneCE[3];
+    S.mixLim = s->mixLim;
     S.winst = s->instanced ? s->winst.as<float4>() : nullptr;
     S.gBits = s->gBits;
     return S;
@@ -3139,11 +3209,14 @@ int pt_scene_build_bvh_ex(pt_scene* s, int flags, void* stream) {
             for (int a = 0; a < 3; a++) { mn[a] = b6[a]; mx[a] = b6[3 + a]; }
         }
         float e = 0.0f;
+        double m = 0.0;
         for (int a = 0; a < 3; a++) {
             s->sceneCE[a] = 0.5f * (mn[a] + mx[a]);
             e = std::fmax(e, mx[a] - mn[a]);
+            m = std::max({m, std::fabs((double)mn[a]), std::fabs((double)mx[a]), (double)mx[a] - (double)mn[a]});
         }
         s->sceneCE[3] = e;
+        s->mixLim = mixLimit(m);
     }
     if (n > 1 && stackFor(s->depth) < 0) return fail(PT_ERR_STATE, "BVH too deep");
     if (s->wideReady && wideStackFor(s->wideDepth) < 0) return fail(PT_ERR_STATE, "wide BVH too deep");

@@ -52,3 +52,39 @@ __device__ __forceinline__ float uniformOf(uint32_t x) { return __builtin_fmaf((
 // round(2u - 1) = 2 * round(u - 0.5): one FMA instead of a subtract and a multiply.  Checked for
 // every u = uniformOf(x) (tools/micro/rcp_check.hip).
 __device__ __forceinline__ float centered2Of(float u) { return __builtin_fmaf(u, 2.0f, -1.0f); }
+
+// The wide NODE step's plane distances t = q * a + c for a quantised plane byte q.  One
+// v_perm_b32 turns two plane bytes into two fp16 denormals 0x00qq = q * 2^-24 (the zero-byte
+// selector 0x0c fills the high bytes), and v_fma_mix_f32 multiplies such an fp16 half (widened
+// exactly) by aS = a * 2^24 and adds c with one rounding: the same exact product-sum as
+// fma((float)q, a, c), so the same result bit for bit whenever aS is finite (the kernels' fp16
+// denormals are on: amdhsa_float_denorm_mode_16_64 3).  Two planes per v_perm instead of one
+// v_cvt_f32_ubyte each.  tools/micro/fmamix_check.hip compares the two forms on the GPU (every q,
+// 2^32 random (q, a, c), denormal / overflow edges; tests/test_gpu_math.py).
+__device__ __forceinline__ uint32_t planePairLo(uint32_t bytes4) { return __builtin_amdgcn_perm(0u, bytes4, 0x0c010c00u); }
+__device__ __forceinline__ uint32_t planePairHi(uint32_t bytes4) { return __builtin_amdgcn_perm(0u, bytes4, 0x0c030c02u); }
+// (The low half as a plain conversion the compiler folds into v_fma_mix_f32 and schedules freely;
+// the high half in asm: with both halves of one register converted, the compiler would widen them
+// as a pair with two v_cvt_f32_f16 instead.)
+__device__ __forceinline__ float fmaMixLo(uint32_t h2, float aS, float c) {
+    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(h2 & 0xffffu)), aS, c);
+}
+__device__ __forceinline__ float fmaMixHi(uint32_t h2, float aS, float c) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(aS), "v"(c));
+    return r;
+}
+// v_max3_f32 / v_min3_f32 on fmaMixHi results: an fmaxf / fminf on an asm output makes the compiler
+// quiet it first (one v_max_f32 x, x, x per operand: it cannot know the value is canonical).  The
+// plain instructions give the same result here (IEEE mode: a quiet NaN operand is ignored, the
+// fma results are never signalling).
+__device__ __forceinline__ float max3Raw(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float min3Raw(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}

@@ -32,3 +32,19 @@ def test_fast_reciprocal_equals_ieee_division_for_every_input():
     assert res["uniform_fma_mismatches"] == 0
     assert res["centered2_fma_mismatches"] == 0
     assert out.returncode == 0
+
+
+@pytest.mark.gpu
+def test_fp16_denormal_plane_arithmetic_is_exact():
+    """The wide NODE step's plane distances (pt_math.hpp planePairLo/Hi + fmaMixLo/Hi: v_perm_b32
+    into fp16 denormals q * 2^-24, v_fma_mix_f32 with the scale times 2^24) equal
+    fma((float)q, a, c) bit for bit: every plane byte, 2^32 random (byte, scale, offset) cases and
+    the denormal / overflow edges (tools/micro/fmamix_check.hip).  Tolerance: 0 ulp."""
+    check = os.path.join(REPO, "tools", "micro", "fmamix_check")
+    assert os.path.exists(check), "tools/micro/fmamix_check not built (make -C path-tracer-cuda-opengl_amd)"
+    out = subprocess.run([check], capture_output=True, text=True, timeout=120)
+    assert out.returncode in (0, 1), out.stderr
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["random_tests"] == 2 ** 32
+    assert res["random_mismatches"] == 0 and res["edge_mismatches"] == 0
+    assert out.returncode == 0

@@ -299,3 +299,33 @@ def test_wide_render_far_camera(pt, orc, gpu, wb):
                                  nthreads=8)
     assert np.array_equal(bits(rgb), bits(ref))
     assert st.rays == rst.rays and st.rays > w * h * 4
+
+
+@pytest.mark.parametrize("name", ["cornell", "bunny_cornell"])
+def test_wide_trace_near_axis_directions(pt, orc, gpu, wb, name):
+    """The MIX plane arithmetic (wideHits<MIX>: fp16-denormal planes, scale s * 2^24 * inv) is exact
+    while |inv| <= DevScene::mixLim; rays with a finite |1/d| component beyond it take the
+    reference-order query (mixUnsafe), and exactly zero components (|inv| = inf) stay on the wide
+    path.  Axis-parallel and nearly axis-parallel rays (components 0, +-2^-100, +-2^-126, denormal)
+    through the Cornell box's axis-aligned walls, from inside the box and aimed at vertices, keep
+    the reference's hits bit for bit."""
+    p = pt.Preset(name, 32, 32)
+    objs = p.objects
+    lo = objs["v"][:, :3].min(0)
+    hi = objs["v"][:, :3].max(0)
+    rng = np.random.default_rng(5)
+    n = 8192
+    o = (lo + (hi - lo) * rng.uniform(0.05, 0.95, (n, 3))).astype(np.float32)
+    k = rng.integers(0, len(objs), n)
+    tgt = objs["v"][k].reshape(-1, 3, 3)[np.arange(n), rng.integers(0, 3, n)]
+    d = (tgt - o).astype(np.float32)
+    tiny = np.array([0.0, 2.0 ** -100, -(2.0 ** -100), 2.0 ** -126, -(2.0 ** -140), 1e-42], np.float32)
+    for i in range(n):   # one or two components replaced by a tiny value per ray
+        ax = rng.permutation(3)[: 1 + (i % 2)]
+        d[i, ax] = tiny[rng.integers(0, len(tiny), len(ax))]
+    d[d.sum(1) == 0, 2] = 1.0
+    rays = np.concatenate([o, d], 1).astype(np.float32)
+    hits, st, ref, rst = trace_both(pt, orc, gpu, wb, objs, p.materials, rays)
+    assert_hits_equal(hits, ref)
+    assert ref["hit"].sum() > n // 2
+    assert st.rays == len(rays)
