@@ -121,12 +121,19 @@ __device__ __forceinline__ float3 normalize3(float3 v) {
 __device__ __forceinline__ float3 xyz(float4 v) { return f3(v.x, v.y, v.z); }
 
 // ------------------------------------------------------------------------ XORWOW
+#ifndef PT_XORWOW_BITOP3
+#define PT_XORWOW_BITOP3 1
+#endif
 struct Xorwow {
     uint32_t d, v0, v1, v2, v3, v4;
     __device__ __forceinline__ uint32_t next() {   // curand(curandStateXORWOW*)
         uint32_t t = v0 ^ (v0 >> 2);
         v0 = v1; v1 = v2; v2 = v3; v3 = v4;
+#if PT_XORWOW_BITOP3   // the three-way XOR in one v_bitop3_b32 (gfx950): six VALU per draw instead of seven
+        v4 = __builtin_amdgcn_bitop3_b32(v4, v4 << 4, t ^ (t << 1), 0x96);
+#else
         v4 = (v4 ^ (v4 << 4)) ^ (t ^ (t << 1));
+#endif
         d += 362437u;
         return v4 + d;
     }
