@@ -1,5 +1,6 @@
 """Render one frame (profiling target).  usage: python tools/one_frame.py [c2|c3|c5] [spp] [compat|sample] [chunk]
-REPEAT=n renders n frames (later launches use the measured tile costs) and reports the fastest."""
+REPEAT=n renders n frames (later launches use the measured tile costs) and reports the fastest.
+NPARTS=n PART=k render one rank's share of an n-GPU frame (8-row stripes, stripe s on part s % n)."""
 import hashlib
 import json
 import os
@@ -17,7 +18,8 @@ rng = ptamd.RNG_SAMPLE if len(sys.argv) > 3 and sys.argv[3] == "sample" else pta
 chunk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg])
 scene = ptamd.Scene(p.objects, p.materials)
-film = ptamd.Film(p.width, p.height, 1)
+film = ptamd.Film(p.width, p.height, 1, stripe_height=8, n_parts=int(os.environ.get("NPARTS", "1")),
+                  part=int(os.environ.get("PART", "0")))
 best = None
 digest = None
 for _ in range(int(os.environ.get("REPEAT", "1"))):   # later launches use measured tile costs
