@@ -845,6 +845,8 @@ struct RenderParams {
     int kernel;                               // PT_KERNEL_*
     unsigned long long* waveTimes;            // optional (PT_WAVE_TIMES): {start, end, tile|xcc<<32} per wave
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
+    const uint32_t* tileXY;                   // sample mode: tile of each launch slot as tx | ty << 16 (the order decoded)
+    int nblocksShift;                         // sample mode: log2(nblocks) when a power of two, else -1
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
     int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
     // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples.  Each
@@ -1301,14 +1303,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             poolBase += take_;                                                                    \
             poolLeft -= take_;                                                                    \
             const uint32_t g0_ = base_ >> 6, off_ = base_ & 63u;                                  \
-            const uint32_t slotA_ = g0_ / (uint32_t)Q_.nblocks, blkA_ = g0_ - slotA_ * (uint32_t)Q_.nblocks; \
+            const uint32_t slotA_ = Q_.nblocksShift >= 0 ? g0_ >> Q_.nblocksShift : g0_ / (uint32_t)Q_.nblocks; \
+            const uint32_t blkA_ = g0_ - slotA_ * (uint32_t)Q_.nblocks;                           \
             const bool wrap_ = blkA_ + 1u == (uint32_t)Q_.nblocks;                                  \
             const uint32_t slotB_ = wrap_ ? slotA_ + 1u : slotA_, blkB_ = wrap_ ? 0u : blkA_ + 1u; \
             const uint32_t nslots_ = (uint32_t)Q_.ntiles;                                          \
-            const uint32_t tA_ = slotA_ < nslots_ ? (Q_.tileOrder ? (uint32_t)Q_.tileOrder[slotA_] : slotA_) : 0u; \
-            const uint32_t tB_ = slotB_ < nslots_ ? (Q_.tileOrder ? (uint32_t)Q_.tileOrder[slotB_] : slotB_) : 0u; \
-            const uint32_t tyA_ = tA_ / (uint32_t)Q_.tiles_x, txA_ = tA_ - tyA_ * (uint32_t)Q_.tiles_x; \
-            const uint32_t tyB_ = tB_ / (uint32_t)Q_.tiles_x, txB_ = tB_ - tyB_ * (uint32_t)Q_.tiles_x; \
+            /* the slots' tiles, decoded once per launch order (tileXYKernel): no divisions here */ \
+            const uint32_t xyA_ = slotA_ < nslots_ ? Q_.tileXY[slotA_] : 0u;                      \
+            const uint32_t xyB_ = slotB_ < nslots_ ? Q_.tileXY[slotB_] : 0u;                      \
+            const uint32_t txA_ = xyA_ & 0xffffu, tyA_ = xyA_ >> 16;                              \
+            const uint32_t txB_ = xyB_ & 0xffffu, tyB_ = xyB_ >> 16;                              \
             const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));                 \
             if (needTask && k_ < take_) {                                                         \
                 if (base_ + k_ >= Q_.ntasks) {                                                     \
@@ -1863,6 +1867,16 @@ __global__ __launch_bounds__(256) void resolveKernel(const float* __restrict__ s
 
 // Longest-first launch order on the device: keys ~cost (ascending = cost descending) and tile ids,
 // then a stable radix sort (pt_sort.hip): equal costs keep ascending tile ids.
+// Sample mode: each launch slot's tile as tx | ty << 16 (`order` = the longest-first launch order,
+// null = identity), so the task hand-out does no divisions per take.
+__global__ __launch_bounds__(256) void tileXYKernel(const uint32_t* __restrict__ order, int n, int tilesX, uint32_t* xy) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = order ? order[i] : (uint32_t)i;
+    const uint32_t ty = t / (uint32_t)tilesX;
+    xy[i] = (t - ty * (uint32_t)tilesX) | (ty << 16);
+}
+
 __global__ __launch_bounds__(256) void tileKeyKernel(const unsigned* __restrict__ cost, uint32_t* keys, uint32_t* ids,
                                                      int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2478,6 +2492,8 @@ struct pt_film {
     DevBuf state;   // 6 x npix uint32 (SoA)
     DevBuf jumps;   // XORWOW jump matrices (for pt_film_reset)
     DevBuf tileCost, tileOrder;   // measured per-tile cost of the last launch; LPT launch order
+    DevBuf tileXY, tileXYId;      // sample mode: tileOrder decoded (tileXYKernel), and the identity order decoded
+    bool haveXYId = false;
     DevBuf tileKeys, tileKeys2, tileIds, sortTemp;   // the order's radix sort on the device
     bool haveOrder = false;
     int framesSinceCost = 0;      // sample mode: frames rendered since the tile costs were last measured
@@ -3609,7 +3625,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     const int stack = kernel == PT_KERNEL_WIDE ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
     const size_t ntl = (size_t)std::max(1, P.ntiles);
     if (!f->tileCost.p) {
-        if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4))) return rc;
+        if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4)) ||
+            (rc = devAlloc(f->tileXY, ntl * 4)) || (rc = devAlloc(f->tileXYId, ntl * 4)))
+            return rc;
         f->haveOrder = false;
     }
     const bool lpt = !(opts && (opts->flags & PT_RENDER_IDENTITY_ORDER));
@@ -3675,6 +3693,17 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     }
     P.tileCost = f->tileCost.as<unsigned>();
     P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
+    P.tileXY = nullptr;
+    P.nblocksShift = -1;
+    if (sample) {   // the launch order decoded per slot (tileXYKernel; the ordered table follows each sort)
+        P.nblocksShift = (P.nblocks & (P.nblocks - 1)) == 0 ? __builtin_ctz((unsigned)P.nblocks) : -1;
+        if (!P.tileOrder && !f->haveXYId) {
+            tileXYKernel<<<(unsigned)((ntl + 255) / 256), 256, 0, st>>>(nullptr, (int)ntl, P.tiles_x, f->tileXYId.as<uint32_t>());
+            HIP_TRY(hipGetLastError());
+            f->haveXYId = true;
+        }
+        P.tileXY = P.tileOrder ? f->tileXY.as<uint32_t>() : f->tileXYId.as<uint32_t>();
+    }
     P.prioTiles = (P.tileOrder && !sample) ? envInt("PT_PRIO_TILES", 1024) : 0;
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
@@ -3720,6 +3749,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         HIP_TRY(hipGetLastError());
         HIP_TRY(pt::radixSortPairs(f->sortTemp.p, &tbytes, f->tileKeys.as<uint32_t>(), f->tileKeys2.as<uint32_t>(),
                                    f->tileIds.as<uint32_t>(), f->tileOrder.as<uint32_t>(), ntl, 32, st));
+        tileXYKernel<<<(unsigned)((nt + 255) / 256), 256, 0, st>>>(f->tileOrder.as<uint32_t>(), nt, P.tiles_x,
+                                                                   f->tileXY.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
         f->haveOrder = true;
     }
     if (P.waveTimes) {
