@@ -1135,6 +1135,7 @@ __device__ __forceinline__ KArgs kargs() {
 }
 
 typedef const __attribute__((address_space(4))) float KFloat;
+typedef const __attribute__((address_space(4))) uint32_t* KU32;   // read-only launch tables, scalar loads
 __device__ __forceinline__ float3 ld3(const __attribute__((address_space(4))) float3& v) {
     KFloat* f = (KFloat*)&v;
     return f3(f[0], f[1], f[2]);
@@ -1309,8 +1310,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             const uint32_t slotB_ = wrap_ ? slotA_ + 1u : slotA_, blkB_ = wrap_ ? 0u : blkA_ + 1u; \
             const uint32_t nslots_ = (uint32_t)Q_.ntiles;                                          \
             /* the slots' tiles, decoded once per launch order (tileXYKernel): no divisions here */ \
-            const uint32_t xyA_ = slotA_ < nslots_ ? Q_.tileXY[slotA_] : 0u;                      \
-            const uint32_t xyB_ = slotB_ < nslots_ ? Q_.tileXY[slotB_] : 0u;                      \
+            /* (scalar loads through the constant address space: a vector load here would wait   \
+               out the accumulator atomics a finishing lane has just issued -- vmcnt counts every \
+               vector memory operation in issue order) */                                        \
+            const uint32_t xyA_ = slotA_ < nslots_ ? ((KU32)Q_.tileXY)[__builtin_amdgcn_readfirstlane(slotA_)] : 0u; \
+            const uint32_t xyB_ = slotB_ < nslots_ ? ((KU32)Q_.tileXY)[__builtin_amdgcn_readfirstlane(slotB_)] : 0u; \
             const uint32_t txA_ = xyA_ & 0xffffu, tyA_ = xyA_ >> 16;                              \
             const uint32_t txB_ = xyB_ & 0xffffu, tyB_ = xyB_ >> 16;                              \
             const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));                 \
