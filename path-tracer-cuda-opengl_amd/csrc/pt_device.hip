@@ -3616,17 +3616,20 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     // together with nodeMin 8 (C3 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 -> 1,180 against 8 / 12).
     const bool sampleRng = rng == PT_RNG_SAMPLE;
     // sample mode, wide kernel (speculative traversal): LEAF at 28 waiting lanes, SHADE at 28
-    // (C3 @256 spp 148.4 -> 145.0 ms vs 24 / 32; C5 @64 75.9 -> 74.5; C2 @1024 135.4 -> 134.5)
+    // (C3 @256 spp 148.4 -> 145.0 ms vs 24 / 32; C5 @64 75.9 -> 74.5; C2 @1024 135.4 -> 134.5);
+    // deep wide trees (a 16+ entry stack: C5's 1.04 M triangles) at 24 / 24 (round 3 close: C5 @64
+    // 67.1 -> 65.1 ms, median of 5; C3 at 24 / 24 is 1 % slower, so shallow trees keep 28 / 28)
     const bool wideSample = sampleRng && kernel == PT_KERNEL_WIDE;
+    const int stack = kernel == PT_KERNEL_WIDE ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
+    const int wideBatch = stack >= 16 ? 24 : 28;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
-                                                 : envInt("PT_LEAF_BATCH", wideSample ? 28 : (sampleRng ? 24 : 20));
+                                                 : envInt("PT_LEAF_BATCH", wideSample ? wideBatch : (sampleRng ? 24 : 20));
     // compat mode: a NODE step with fewer than nodeMin lanes yields to the larger of the waiting
     // LEAF / SHADE groups (C3 compat 1,620 -> 1,517 ms at 8; 4: 1,548, 16: 1,671, 32: 1,989)
     P.nodeMin = std::getenv("PT_NODE_MIN") ? std::atoi(std::getenv("PT_NODE_MIN")) : 8;
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
-                                                   : envInt("PT_SHADE_BATCH", wideSample ? 28 : (sampleRng ? 32 : 12));
+                                                   : envInt("PT_SHADE_BATCH", wideSample ? wideBatch : (sampleRng ? 32 : 12));
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
-    const int stack = kernel == PT_KERNEL_WIDE ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
     const size_t ntl = (size_t)std::max(1, P.ntiles);
     if (!f->tileCost.p) {
         if ((rc = devAlloc(f->tileCost, ntl * 4)) || (rc = devAlloc(f->tileOrder, ntl * 4)) ||
