@@ -64,30 +64,76 @@ CONFIG_SPP = {"c4": 4096}
 STRIPE = 8
 
 
-def cpu_baseline(preset, budget_s: float = 12.0) -> dict:
+def cpu_facts() -> dict:
+    """The host the CPU baseline ran on: nproc (os.cpu_count(): every CPU of the machine), the CPUs
+    this process may run on (affinity mask), the cgroup CPU quota if one is set, and the CPU model
+    (/proc/cpuinfo).  On the GPU pool a 1-GPU box is a share of a larger machine: os.cpu_count()
+    counts the whole machine, the share (affinity / quota) is what a process can use."""
+    nproc = os.cpu_count() or 1
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):   # cgroup v2: "<quota> <period>" or "max <period>"
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = allowed if quota is None else max(1, min(allowed, int(quota)))
+    return {"nproc": nproc, "cpus_allowed": allowed, "cgroup_cpu_quota": quota, "cpu_model": model,
+            "usable_cpus": usable}
+
+
+def cpu_baseline(preset, budget_s: float = 12.0, gpu_ref=None) -> dict:
     """Oracle (scalar C++ port of the reference path, std::thread over rows) on a bounded sample:
-    the full frame at 1 spp per pass, passes repeated until `budget_s` of CPU work."""
+    the full frame at 1 spp per pass, passes repeated until `budget_s` of CPU work.  One thread per
+    CPU this process may use (the affinity mask / cgroup quota: on the GPU pool the box's share of
+    its machine, whose nproc is larger -- both are recorded); the host's timing in the reference is
+    std::clock around render (main.cu:469-476).  Beside the rate: the CPU traversal's node visits
+    and primitive tests per ray (binary LBVH, the reference's order) and the GPU's counts for the
+    same scene (reference-order kernel and the wide kernel), as BASELINE.md section 4 asks."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    facts = cpu_facts()
+    threads = int(os.environ.get("PT_CPU_THREADS", "0")) or facts["usable_cpus"]
     w, h = preset.width, preset.height
     nodes = oracle.build_lbvh(preset.objects, oracle.morton_keys(preset.objects), tight=True)
     rows = np.arange(h, dtype=np.int32)
     states = oracle.film_states(1, w, rows)
     cam = ptamd.camera_to_array(preset.camera)
-    rays, passes, t0 = 0, 0, time.perf_counter()
+    rays = visits = tris = sphs = 0
+    passes, t0 = 0, time.perf_counter()
     while True:
         _, st = oracle.render(preset.objects, preset.materials, nodes, cam, w, h, rows, 1, preset.max_depth,
                               states, nthreads=threads)
         rays += st.rays
+        visits += st.node_visits
+        tris += st.tri_tests
+        sphs += st.sphere_tests
         passes += 1
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    return {"value": rays / el / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": f"{preset.name} {w}x{h}, {passes} pass(es) of 1 spp depth {preset.max_depth} "
-                      f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads"}
+    out = {"value": rays / el / 1e6, "unit": "Mray/s", "cores": threads, "threads": threads, "kind": "port",
+           "sample": f"{preset.name} {w}x{h}, {passes} pass(es) of 1 spp depth {preset.max_depth} "
+                     f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads",
+           "per_ray": {"cpu_node_visits": visits / max(rays, 1), "cpu_prim_tests": (tris + sphs) / max(rays, 1)}}
+    out.update(facts)
+    if gpu_ref:
+        out["per_ray"].update(gpu_ref)
+    return out
 
 
 def build_id() -> str:
@@ -401,7 +447,14 @@ def main() -> None:
             del dyn
         out["scene_build"] = scene_build
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(ptamd.Preset(name) if instanced else preset)
+            gpu_ref = None if instanced else {
+                "gpu_reference_order_node_visits": ref_st.node_visits / max(ref_st.rays, 1),
+                "gpu_reference_order_prim_tests": (ref_st.tri_tests + ref_st.sphere_tests) / max(ref_st.rays, 1),
+                "gpu_wide_node_visits": st.node_visits / max(st.rays, 1),
+                "gpu_wide_prim_tests": (st.tri_tests + st.sphere_tests) / max(st.rays, 1),
+                "note": "node visits: binary LBVH nodes (CPU, reference-order GPU kernel) vs compressed 8-wide "
+                        "nodes (wide kernel); CPU at 1 spp (bounded sample), GPU over the whole frame"}
+            out["cpu_baseline"] = cpu_baseline(ptamd.Preset(name) if instanced else preset, gpu_ref=gpu_ref)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

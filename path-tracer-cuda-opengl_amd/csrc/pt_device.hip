@@ -38,9 +38,10 @@
 
 using pt::fail;
 
-namespace pt {   // pt_sort.hip
-hipError_t radixSortPairs(void* temp, size_t* temp_bytes, const uint32_t* codes_in, uint32_t* codes_out,
-                          const uint32_t* ids_in, uint32_t* ids_out, size_t n, int bits, hipStream_t stream);
+#include "pt_prims.hpp"   // radixSortPairs (pt_sort.hip)
+
+namespace pt {
+int launchCompatWide(int stack, const void* params, hipStream_t st);   // pt_compat.hip
 }
 
 #define HIP_TRY(expr)                                                                        \
@@ -417,6 +418,43 @@ __device__ __forceinline__ void wideTest(const Prim& q, float3 o, float3 d, floa
             }
         }
     }
+}
+
+// wideTest's decisions on a primitive another lane tested (the wave-cooperative LEAF step): t from
+// primHitAny, key = its rank | kSphereBit for a sphere, blo = its exact leaf box's entry distance
+// (aabb::hit with tmax = inf) or -1 when that box is missed (an entry is >= tmin > 0).  Applied in
+// the group's order, the same updates of closest / best / bestLo / redo as wideTest.
+template <bool SPH>
+__device__ __forceinline__ void wideMerge(float t, uint32_t key, float blo, float& closest, int& best, float& bestLo,
+                                          bool leafBoxes, bool& redo) {
+    if (t >= 0.0f) {
+        const bool sph = SPH && (key & kSphereBit) != 0u;
+        const int k = (int)(key & kPrimMask);
+        const bool none = best < 0, bSph = SPH && (best & (int)kSphereBit) != 0;
+        const int bk = SPH ? best & (int)kPrimMask : best;
+        const bool tie = sph ? (none || !bSph || k > bk) : (!none && !bSph && k < bk);
+        redo = redo || (t >= closest && t < bestLo);
+        if (t < closest || (t == closest && tie)) {
+            bool take = true;
+            float lo = -__builtin_inff();
+            if (leafBoxes) {
+                const bool bh = blo >= 0.0f;
+                take = bh && !(closest < blo);
+                redo = redo || (bh && closest < blo);
+                lo = t < blo ? blo : lo;
+            }
+            if (take) {
+                closest = t;
+                best = k | (sph ? (int)kSphereBit : 0);
+                bestLo = lo;
+            }
+        }
+    }
+}
+
+// Lanes below this one whose bit is set in m (v_mbcnt_lo / v_mbcnt_hi).
+__device__ __forceinline__ __attribute__((unused)) uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // One compressed 8-wide node (five 16-B words, layout in host/pt_wide8.cpp) against the ray:
@@ -846,7 +884,7 @@ struct RenderParams {
     unsigned long long* waveTimes;            // optional (PT_WAVE_TIMES): {start, end, tile|xcc<<32} per wave
     const int* tileOrder;                     // launch order of tiles (longest first), or null = identity
     const uint32_t* tileXY;                   // sample mode: tile of each launch slot as tx | ty << 16 (the order decoded)
-    int nblocksShift;                         // sample mode: log2(nblocks) when a power of two, else -1
+    int nblocksShift;                         // sample mode: log2(ngroups) when a power of two, else -1
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
     int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
     // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples.  Each
@@ -855,10 +893,15 @@ struct RenderParams {
     // (blockFixed), with atomics: integer addition is exact and order-free, so the image does
     // not depend on scheduling or on the stripe partition.  pixAcc[4 * pixel] = {x, y, z, rays}.
     int nblocks, block;
+    // A task covers `group` consecutive summation blocks of one pixel (`span` = group x block samples;
+    // ngroups spans per pixel): each block's fixed-point sum is added into the lane's LDS partial,
+    // and the task adds the partial to the pixel's accumulator once (3 global atomics per task, not
+    // per block).  The fixed-point additions are exact and order-free: the image does not change.
+    int group, span, ngroups;
     unsigned long long* pixAcc;
     unsigned* taskCounter;                    // next task (zeroed before the launch)
     uint32_t* stackSpill;                     // sample mode, STACK > 32: stack entries >= 32 (per wave slot, lane)
-    uint32_t ntasks;                          // tile slots x nblocks x 64
+    uint32_t ntasks;                          // tile slots x ngroups x 64
     int nwaves;                               // persistent waves launched
     uint32_t seed0, seed1;
     uint32_t sampleBase;                      // sample mode: index of the frame's first sample
@@ -885,6 +928,12 @@ __device__ __forceinline__ float fixedToFloat(unsigned long long a) { return (fl
 // that measure tile costs (`cost`: the input of the next launches' longest-first order) -- its ray
 // count; no-return atomics (device scope: 4 of them per task cost 5 % of a C3 frame, so the ray
 // counts are taken on one frame in eight).
+__device__ __forceinline__ __attribute__((unused)) void addFixed1(unsigned long long* acc, unsigned long long v) {
+#if PT_AB_NO_ATOMICS
+    return;
+#endif
+    __hip_atomic_fetch_add(acc, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void addBlock(unsigned long long* acc, float3 sum, uint32_t rays, bool cost) {
 #if PT_AB_NO_ATOMICS
     return;
@@ -1082,6 +1131,13 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #define PT_TASK_POOL 64
 #endif
 constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
+#ifndef PT_TASK_GROUPS
+#define PT_TASK_GROUPS 0   // wide sample kernels: tasks of several summation blocks (LDS partials; measured slower)
+#endif
+#ifndef PT_TASK_BLOCKS
+#define PT_TASK_BLOCKS 2
+#endif
+constexpr int kTaskBlocks = PT_TASK_BLOCKS;   // sample mode: summation blocks per task (PT_TASK_BLOCKS env overrides)
 // Occupancy target of the wavefront kernel (waves per SIMD; 6 = at most 80 VGPRs).  The LDS
 // stack (STACK x 256 B per wave, 160 KB per CU) allows 6 / 5 / 4 / 3 / 2 waves per SIMD at
 // STACK 24 / 32 / 48 / 64 / 80, so deeper trees keep a larger register budget.  Compat tile
@@ -1106,6 +1162,12 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #endif
 #ifndef PT_MIX_CHECK
 #define PT_MIX_CHECK 1   // (A/B timing only: 0 drops the per-ray mixUnsafe test -- not exact for near-axis rays)
+#endif
+#ifndef PT_LEAF_COOP
+#define PT_LEAF_COOP 0   // wide kernels (not instanced): wave-cooperative LEAF steps, one (lane, primitive) pair per lane
+#endif
+#ifndef PT_LEAF_COOP_CAP
+#define PT_LEAF_COOP_CAP 2   // pairs a lane offers per cooperative LEAF step (1-3)
 #endif
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
@@ -1169,12 +1231,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     constexpr int SPECN = (WIDE && !INST) ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
     __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
+    // wave-cooperative LEAF steps: the step's queue of (owner lane, primitive) pairs
+    constexpr bool COOP = WIDE && !INST && PT_LEAF_COOP != 0;
+    __shared__ uint32_t leafQ[COOP ? kWave : 1];
+    if constexpr (COOP) leafQ[threadIdx.x] = 0u;   // (every entry is a valid pair from here on)
     // instanced scenes: the lane's world ray {o, d} while it is inside an instance
     __shared__ float wray[INST ? 6 * kWave : 1];
     // sample mode: the lane's task {pixel col | local row << 16, next sample, end sample, rays}.
     // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
     // in four VGPRs carried through every step.
     __shared__ uint4 taskState[SAMPLE ? kWave : 1];
+    // sample mode, tasks of several blocks: the task's closed blocks so far, per lane (x, y, z)
+    // (wide kernels; the binary ones take one block per task and keep their LDS for the stack)
+    constexpr bool GROUPS = PT_TASK_GROUPS && SAMPLE && WIDE && STACK <= 16;   // (STACK 24: the LDS would cap occupancy)
+    __shared__ unsigned long long accPart[GROUPS ? 3 * kWave : 1];
+    if constexpr (GROUPS) {
+        accPart[threadIdx.x] = 0ull; accPart[kWave + threadIdx.x] = 0ull; accPart[2 * kWave + threadIdx.x] = 0ull;
+    }
     const int lane = threadIdx.x;
     // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
@@ -1304,9 +1377,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             poolBase += take_;                                                                    \
             poolLeft -= take_;                                                                    \
             const uint32_t g0_ = base_ >> 6, off_ = base_ & 63u;                                  \
-            const uint32_t slotA_ = Q_.nblocksShift >= 0 ? g0_ >> Q_.nblocksShift : g0_ / (uint32_t)Q_.nblocks; \
-            const uint32_t blkA_ = g0_ - slotA_ * (uint32_t)Q_.nblocks;                           \
-            const bool wrap_ = blkA_ + 1u == (uint32_t)Q_.nblocks;                                  \
+            const uint32_t slotA_ = Q_.nblocksShift >= 0 ? g0_ >> Q_.nblocksShift : g0_ / (uint32_t)Q_.ngroups; \
+            const uint32_t blkA_ = g0_ - slotA_ * (uint32_t)Q_.ngroups;                           \
+            const bool wrap_ = blkA_ + 1u == (uint32_t)Q_.ngroups;                                  \
             const uint32_t slotB_ = wrap_ ? slotA_ + 1u : slotA_, blkB_ = wrap_ ? 0u : blkA_ + 1u; \
             const uint32_t nslots_ = (uint32_t)Q_.ntiles;                                          \
             /* the slots' tiles, decoded once per launch order (tileXYKernel): no divisions here */ \
@@ -1329,9 +1402,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     if (c_ < Q_.width && r_ < Q_.nrows) {                                           \
                         needTask = false;                                                         \
                         got = true;                                                               \
-                        const uint32_t s0_ = (hi_ ? blkB_ : blkA_) * (uint32_t)Q_.block;          \
+                        const uint32_t s0_ = (hi_ ? blkB_ : blkA_) * (uint32_t)Q_.span;           \
                         taskState[lane] = make_uint4((uint32_t)c_ | ((uint32_t)r_ << 16), s0_,     \
-                                                     min(s0_ + (uint32_t)Q_.block, (uint32_t)Q_.spp), 0u); \
+                                                     min(s0_ + (uint32_t)Q_.span, (uint32_t)Q_.spp), 0u); \
                         sum = f3(0.0f, 0.0f, 0.0f);                                               \
                     }                                                                             \
                 }                                                                                 \
@@ -1344,9 +1417,30 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // are live, measured 2.6 % slower), and the lane asks for its next task.
 #define PT_FINISH_TASK(ts)                                                                          \
     do {                                                                                          \
-        addBlock(kargs()->pixAcc + 4 * (size_t)(((ts).x >> 16) * (uint32_t)kargs()->width + ((ts).x & 0xffffu)), \
-                 sum, (ts).w + 1u, kargs()->measureCost != 0);                                    \
+        unsigned long long* acc_ = kargs()->pixAcc + 4 * (size_t)(((ts).x >> 16) * (uint32_t)kargs()->width + ((ts).x & 0xffffu)); \
+        if constexpr (GROUPS) {   /* the task's earlier blocks wait in the lane's LDS partial */ \
+            addFixed1(acc_ + 0, accPart[lane] + blockFixed(sum.x));                               \
+            addFixed1(acc_ + 1, accPart[kWave + lane] + blockFixed(sum.y));                       \
+            addFixed1(acc_ + 2, accPart[2 * kWave + lane] + blockFixed(sum.z));                   \
+            if (kargs()->measureCost) addFixed1(acc_ + 3, (unsigned long long)((ts).w + 1u));     \
+            accPart[lane] = 0ull; accPart[kWave + lane] = 0ull; accPart[2 * kWave + lane] = 0ull;   \
+        } else {                                                                                  \
+            addBlock(acc_, sum, (ts).w + 1u, kargs()->measureCost != 0);                          \
+        }                                                                                         \
         needTask = true;                                                                          \
+    } while (0)
+    // Sample mode, tasks of several blocks: a block that is not the task's last one closes into the
+    // lane's LDS partial (exact 64-bit additions), and the next block's sum starts from zero.
+#define PT_CLOSE_BLOCK(y_)                                                                          \
+    do {                                                                                          \
+        const auto& Q_ = *kargs();                                                                \
+        if (GROUPS && Q_.group > 1 && (Q_.blockShift >= 0 ? ((y_) & (((uint32_t)1 << Q_.blockShift) - 1u)) == 0u \
+                                                 : (y_) % (uint32_t)Q_.block == 0u)) {            \
+            __hip_atomic_fetch_add(&accPart[lane], blockFixed(sum.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+            __hip_atomic_fetch_add(&accPart[kWave + lane], blockFixed(sum.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+            __hip_atomic_fetch_add(&accPart[2 * kWave + lane], blockFixed(sum.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+            sum = f3(0.0f, 0.0f, 0.0f);                                                           \
+        }                                                                                         \
     } while (0)
 #define PT_NEW_PATH()                                                                               \
     do {                                                                                          \
@@ -1382,10 +1476,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 if (got) {
                     uint4 ts = taskState[lane];
                     depthPaths += ts.z - ts.y;
-                    for (; ts.y < ts.z; ts.y++) {
+                    while (ts.y < ts.z) {
                         taskState[lane].y = ts.y;
                         PT_NEW_PATH();
                         sum = add(sum, sky(d, att));
+                        ts.y++;
+                        if (ts.y < ts.z) PT_CLOSE_BLOCK(ts.y);
                     }
                     PT_FINISH_TASK(ts);
                 }
@@ -1592,8 +1688,84 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             // ------------------------------------------------------------------ LEAF
             bool tested = false, sph = false;
             PT_DIAG_ADD(itL, 1u);
-            PT_DIAG_ADD(sPops, (uint32_t)nL);
-            if constexpr (WIDE) {
+            if constexpr (COOP) {
+                // Wave-cooperative LEAF step: the waiting (lane, primitive) pairs are compacted
+                // so that every lane of the wave tests one.  A lane offers the first `cnt` (<= CAP)
+                // primitives of its group in group order; a ballot prefix sum over the lanes gives
+                // each offer its queue slot (the first 64 slots are taken, the rest wait for the
+                // next LEAF step); lane j tests the pair in slot j against its owner's ray (fetched
+                // with ds_bpermute) and hands (t, leaf box, key) back; each owner then merges its
+                // results in group order with wideMerge -- the decisions wideTest makes, in the same
+                // order, so closest / best / window / redo are exactly those of the one-lane tests.
+                constexpr uint32_t CAP = PT_LEAF_COOP_CAP;
+                const uint32_t pc = (uint32_t)__builtin_popcount(tg);
+                const uint32_t cnt = pc < CAP ? pc : CAP;
+                const uint64_t c0 = __ballot(cnt & 1u), c1 = __ballot(cnt & 2u);
+                const uint32_t pre = mbcnt64(c0) + 2u * mbcnt64(c1);
+                const uint32_t total = (uint32_t)__popcll(c0) + 2u * (uint32_t)__popcll(c1);   // (uniform)
+                const uint32_t take = pre >= (uint32_t)kWave ? 0u : min(cnt, (uint32_t)kWave - pre);
+                const uint32_t own = (uint32_t)lane << 26;   // slot entry: owner << 26 | primitive (< 2^26)
+                if (take > 0u) { leafQ[pre] = own | (tgBase + (uint32_t)__builtin_ctz(tg)); tg &= tg - 1u; }
+                if (CAP > 1 && take > 1u) { leafQ[pre + 1u] = own | (tgBase + (uint32_t)__builtin_ctz(tg)); tg &= tg - 1u; }
+                if (CAP > 2 && take > 2u) { leafQ[pre + 2u] = own | (tgBase + (uint32_t)__builtin_ctz(tg)); tg &= tg - 1u; }
+                __syncthreads();   // (one wave per workgroup: orders the slot writes before the reads)
+                const uint32_t nc = total < (uint32_t)kWave ? total : (uint32_t)kWave;
+                PT_DIAG_ADD(sPops, nc);
+                // lanes past the last pair re-test a stale (valid) entry; their results are not read
+                const uint32_t e = leafQ[lane];
+                const int ow = (int)(e >> 26);
+                const float3 ro = f3(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
+                const float3 rd = f3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
+                const float4* w0 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(e & 0x3ffffffu));
+                const Prim q0{w0[0], w0[1], w0[2]};
+                const bool lb = S.nprims > 1;
+                const bool cons = (uint32_t)lane < nc;
+                float rt, rlo = -__builtin_inff();
+                uint32_t rkey;
+                if (kargs()->S.hasSpheres) {   // (uniform)
+                    const bool sph = __float_as_uint(q0.p2.w) != 0u;
+                    rt = primHitAny(q0, sph, ro, rd, 0.001f);
+                    if (lb) {
+                        const float3 rinv = f3(__shfl(inv.x, ow), __shfl(inv.y, ow), __shfl(inv.z, ow));
+                        const SlabHit b = refLeafBox(q0, sph, ro, rinv, 0.001f, __builtin_inff());
+                        rlo = b.hit ? b.lo : -1.0f;   // (a hit's entry is >= tmin > 0)
+                    }
+                    rkey = __float_as_uint(q0.p0.w) | (sph ? kSphereBit : 0u);
+                    sTris += (uint32_t)__popcll(__ballot(cons && !sph));
+                    sSph += (uint32_t)__popcll(__ballot(cons && sph));
+                } else {
+                    rt = primHitAny(q0, false, ro, rd, 0.001f);
+                    if (lb) {
+                        const float3 rinv = f3(__shfl(inv.x, ow), __shfl(inv.y, ow), __shfl(inv.z, ow));
+                        const SlabHit b = refLeafBox(q0, false, ro, rinv, 0.001f, __builtin_inff());
+                        rlo = b.hit ? b.lo : -1.0f;
+                    }
+                    rkey = __float_as_uint(q0.p0.w);
+                    sTris += nc;
+                }
+                bool redo = false;
+                const bool sphScene = kargs()->S.hasSpheres != 0;
+#pragma unroll
+                for (uint32_t r = 0; r < CAP; r++) {
+                    if (__ballot(take > r) == 0) break;
+                    const int src = (int)(pre + r);
+                    const float t = __shfl(rt, src);
+                    const float blo = __shfl(rlo, src);
+                    const uint32_t key = (uint32_t)__shfl((int)rkey, src);
+                    if (take > r) {
+                        if (sphScene) wideMerge<true>(t, key, blo, closest, best, bestLo, lb, redo);
+                        else wideMerge<false>(t, key, blo, closest, best, bestLo, lb, redo);
+                    }
+                }
+                if (redo) oct |= 8u;   // order-dependent candidate: repeat the query in the reference's order
+                if (SPEC && tg == 0u && (oct & 48u)) {   // this group is done: the last parked one is next
+                    oct -= 16u;
+                    const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
+                    tgBase = pend[(2u * c) * kWave + lane];
+                    tg = pend[(2u * c + 1u) * kWave + lane];
+                }
+            } else if constexpr (WIDE) {
+                PT_DIAG_ADD(sPops, (uint32_t)nL);
                 // up to two primitives of the group per step, both records loaded up front
                 uint32_t k0 = 0u, k1 = 0u;
                 const bool h0 = tg != 0u;
@@ -1630,6 +1802,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     tg = pend[(2u * c + 1u) * kWave + lane];
                 }
             } else {
+            PT_DIAG_ADD(sPops, (uint32_t)nL);
             // Every lane tests all of its queued leaves, in order, in this step (the queue then
             // is empty and the lane rejoins NODE steps; measured -4 % vs one leaf per step).
             // The first two queued primitives are loaded together up front (their addresses are
@@ -1713,6 +1886,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                             active = false;
                             PT_FINISH_TASK(ts);
                         } else {
+                            PT_CLOSE_BLOCK(ts.y);
                             newSample = true;
                         }
                     } else {
@@ -1807,7 +1981,30 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK
+#undef PT_CLOSE_BLOCK
 #undef PT_DIAG_ADD
+
+#ifdef PT_TU_COMPAT
+}  // namespace
+
+// pt_compat.hip compiles this file a second time with PT_TU_COMPAT: only the device code above and
+// this launcher of the compat-mode wide kernels (renderKernelWF<S, false, true>), built WITHOUT the
+// -mllvm --enable-post-misched=0 of the main translation unit.  That flag speeds the sample-mode
+// kernels up but slows the compat kernel -- one sequential chain of samples per pixel -- by 3.5 %
+// (DESIGN.md section 6), and it is a per-file option.
+namespace pt {
+int launchCompatWide(int stack, const void* params, hipStream_t st) {
+    const RenderParams& P = *static_cast<const RenderParams*>(params);
+    switch (stack) {
+        case 8: renderKernelWF<8, false, true><<<P.ntiles, kWave, 0, st>>>(P); break;
+        case 16: renderKernelWF<16, false, true><<<P.ntiles, kWave, 0, st>>>(P); break;
+        case 24: renderKernelWF<24, false, true><<<P.ntiles, kWave, 0, st>>>(P); break;
+        default: return -1;
+    }
+    return 0;
+}
+}  // namespace pt
+#else
 
 // Frame epilogue (one lane per pixel).  The frame's linear sum S is the raw compat sum
 // (`nblocks` = 0) or, in sample mode, the block sums added in order.  Accumulating films keep
@@ -2813,7 +3010,7 @@ void launchRenderWide(const RenderParams& P, hipStream_t st) {
         return;
     }
     if (P.pixAcc) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
-    else renderKernelWF<S, false, true><<<P.ntiles, kWave, 0, st>>>(P);
+    else pt::launchCompatWide(S, &P, st);   // (its own translation unit, pt_compat.hip)
 }
 template <int S>
 void launchRender(const RenderParams& P, hipStream_t st) {
@@ -3597,6 +3794,9 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.nblocks = 0;
     P.block = 0;
     P.blockShift = -1;
+    P.group = 1;
+    P.span = 0;
+    P.ngroups = 0;
     P.pixAcc = nullptr;
     P.taskCounter = nullptr;
     P.stackSpill = nullptr;
@@ -3645,10 +3845,15 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         P.block = (opts && opts->chunk > 0) ? opts->chunk : std::max(16, (spp + 63) / 64);
         P.nblocks = (spp + P.block - 1) / P.block;
         P.blockShift = (P.block & (P.block - 1)) == 0 ? __builtin_ctz((unsigned)P.block) : -1;
+        // blocks per task (the simple kernel always takes one)
+        P.group = (!PT_TASK_GROUPS || kernel != PT_KERNEL_WIDE || stack > 16) ? 1   // (renderKernelWF's GROUPS)
+                                                          : std::max(1, std::min(P.nblocks, envInt("PT_TASK_BLOCKS", kTaskBlocks)));
+        P.span = P.group * P.block;
+        P.ngroups = (spp + P.span - 1) / P.span;
         if ((rc = devReserve(f->pixAcc, (size_t)np * 32))) return rc;   // {x, y, z, rays} per pixel
         HIP_TRY(hipMemsetAsync(f->pixAcc.p, 0, (size_t)np * 32, st));
         P.pixAcc = f->pixAcc.as<unsigned long long>();
-        const uint64_t ntasks = (uint64_t)P.ntiles * (uint64_t)P.nblocks * 64u;
+        const uint64_t ntasks = (uint64_t)P.ntiles * (uint64_t)P.ngroups * 64u;
         if (ntasks >= (1ull << 32) - 4096)
             return fail(PT_ERR_INVALID, "sample mode: too many (pixel, block) tasks; raise the block size (chunk)");
         P.ntasks = (uint32_t)ntasks;
@@ -3703,7 +3908,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.tileXY = nullptr;
     P.nblocksShift = -1;
     if (sample) {   // the launch order decoded per slot (tileXYKernel; the ordered table follows each sort)
-        P.nblocksShift = (P.nblocks & (P.nblocks - 1)) == 0 ? __builtin_ctz((unsigned)P.nblocks) : -1;
+        P.nblocksShift = (P.ngroups & (P.ngroups - 1)) == 0 ? __builtin_ctz((unsigned)P.ngroups) : -1;
         if (!P.tileOrder && !f->haveXYId) {
             tileXYKernel<<<(unsigned)((ntl + 255) / 256), 256, 0, st>>>(nullptr, (int)ntl, P.tiles_x, f->tileXYId.as<uint32_t>());
             HIP_TRY(hipGetLastError());
@@ -3796,3 +4001,4 @@ void pt_scene_destroy(pt_scene* s) {
 }
 
 }  // extern "C"
+#endif  // PT_TU_COMPAT

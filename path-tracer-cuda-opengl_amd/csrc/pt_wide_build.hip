@@ -15,12 +15,12 @@
 //    parents' order, slot order -- the host build's breadth-first order -- so the output is
 //    deterministic (the node ids PLOC hands out by atomic counter never reach it).
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_scan.hpp>
 
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 
+#include "pt_prims.hpp"
 #include "pt_wide_dev.hpp"
 
 namespace pt {
@@ -349,12 +349,6 @@ __global__ void wideCountKernel(Tree T, const uint2* __restrict__ items, int m, 
     cnt[i] = make_uint4(internal ? 8u : 0u, prims, internal, 0u);
 }
 
-struct Add3 {
-    __device__ __host__ uint4 operator()(const uint4& a, const uint4& b) const {
-        return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, 0u);
-    }
-};
-
 __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, const uint4* __restrict__ cnt,
                                 const uint4* __restrict__ ofs, uint32_t nodeBase, uint32_t primBase, uint32_t slotCap,
                                 const uint32_t* __restrict__ rootCid, const float4* __restrict__ prims,
@@ -570,13 +564,8 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
     WB_TRY(reserve(cnt_, nn * 16));
     WB_TRY(reserve(ofs_, nn * 16));
     WB_TRY(reserve(misc_, kMiscWords * 4));
-    size_t tb1 = 0, tb2 = 0;
-    WB_TRY(rocprim::exclusive_scan(nullptr, tb1, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, nn,
-                                   rocprim::plus<uint32_t>(), st));
-    WB_TRY(rocprim::exclusive_scan(nullptr, tb2, (const uint4*)nullptr, (uint4*)nullptr, make_uint4(0u, 0u, 0u, 0u), nn,
-                                   Add3(), st));
+    const size_t tb1 = scanScratchBytesU32(nn), tb2 = scanScratchBytesU3(nn);
     WB_TRY(reserve(scanTemp_, tb1 > tb2 ? tb1 : tb2));
-    size_t tbytes = scanTemp_.cap;
     uint32_t* misc = static_cast<uint32_t*>(misc_.p);
     float4* pbox = static_cast<float4*>(pbox_.p);
     uint2* pchild = static_cast<uint2*>(pchild_.p);
@@ -622,7 +611,7 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
             }
             plocMergeKernel<<<blocks(m, tb), tb, 0, st>>>(cid, pbox, pchild, nearest, mIn, (int)m, (int)n, trav, flag, misc);
             WB_TRY(hipGetLastError());
-            WB_TRY(rocprim::exclusive_scan(scanTemp_.p, tbytes, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), st));
+            WB_TRY(exclusiveScanU32(scanTemp_.p, flag, pos, (size_t)m, st));
             plocCompactKernel<<<blocks(m, tb), tb, 0, st>>>(cid, flag, pos, mIn, static_cast<uint32_t*>(cid_[cur ^ 1].p),
                                                             misc + kMiscM + ((pass + 1) & 1));
             WB_TRY(hipGetLastError());
@@ -670,7 +659,7 @@ hipError_t WideDevBuilder::build(const WideDevIn& in, WideDevOut& out, hipStream
         uint4* ofs = static_cast<uint4*>(ofs_.p);
         wideCountKernel<<<blocks(items, tb), tb, 0, st>>>(T, cur2, (int)items, cnt);
         WB_TRY(hipGetLastError());
-        WB_TRY(rocprim::exclusive_scan(scanTemp_.p, tbytes, cnt, ofs, make_uint4(0u, 0u, 0u, 0u), (size_t)items, Add3(), st));
+        WB_TRY(exclusiveScanU3(scanTemp_.p, cnt, ofs, (size_t)items, st));
         wideWriteKernel<<<blocks(items, tb), tb, 0, st>>>(T, cur2, (int)items, cnt, ofs, nodeBase, primBase, slotCap, rootCid,
                                                           in.prims, out.rank, out.nodes, reinterpret_cast<uint4*>(out.wprims),
                                                           static_cast<uint2*>(items_[it ^ 1].p), misc);

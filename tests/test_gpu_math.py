@@ -48,3 +48,17 @@ def test_fp16_denormal_plane_arithmetic_is_exact():
     assert res["random_tests"] == 2 ** 32
     assert res["random_mismatches"] == 0 and res["edge_mismatches"] == 0
     assert out.returncode == 0
+
+
+@pytest.mark.gpu
+def test_hand_written_radix_sort_and_scans():
+    """The build path's device primitives (csrc/pt_sort.hip, replacing rocPRIM): the stable LSD
+    radix sort equals std::stable_sort by key (values carried, inputs untouched) at sizes around its
+    1024-pair tile up to 2^22 pairs, with heavy duplicates and all-equal keys, for 30 / 32 / 8 bits;
+    the decoupled look-back scans (uint32 and the wide build's {x, y, z} uint4 sums) equal the
+    sequential exclusive sums up to 2^23 items (tools/micro/sort_check.hip).  Exact."""
+    check = os.path.join(REPO, "tools", "micro", "sort_check")
+    assert os.path.exists(check), "tools/micro/sort_check not built (make -C path-tracer-cuda-opengl_amd)"
+    out = subprocess.run([check], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "ok"
