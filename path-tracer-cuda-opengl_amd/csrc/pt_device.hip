@@ -552,6 +552,22 @@ __device__ __forceinline__ bool wideFar(float cx, float cy, float cz, float ext,
 }
 __device__ __forceinline__ bool wideFar(const DevScene& S, float3 o) { return wideFar(S.cx, S.cy, S.cz, S.ext, o); }
 
+// Instanced scenes have no reference-order query: a ray whose origin lies beyond the region the
+// planes' margin covers (wideFar) is moved along itself to its entry into the world box grown by one
+// extent on every side -- no geometry lies before that point, and the new origin is within 1.5
+// extents of the centre, inside the region every instanced tree was quantised for (buildInstanced).
+// Returns the distance moved (0 when the ray misses that box or starts inside it).
+__device__ __forceinline__ float instEntry(float cx, float cy, float cz, float ext, float3& o, float3 d, float3 inv) {
+    const float lx = (cx - ext - o.x) * inv.x, hx = (cx + ext - o.x) * inv.x;
+    const float ly = (cy - ext - o.y) * inv.y, hy = (cy + ext - o.y) * inv.y;
+    const float lz = (cz - ext - o.z) * inv.z, hz = (cz + ext - o.z) * inv.z;
+    const float t0 = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fminf(lz, hz));
+    const float t1 = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fmaxf(lz, hz));
+    if (!(t0 > 0.0f) || !(t0 <= t1)) return 0.0f;
+    o = add(o, scale(t0, d));
+    return t0;
+}
+
 // A reciprocal direction component that is finite but larger than `lim` (DevScene::mixLim: a ray
 // nearly parallel to an axis plane) would overflow the MIX plane scale s * 2^24 * inv (wideHits);
 // such a ray takes the reference-order query.  (An infinite component is fine: both forms then
@@ -1336,6 +1352,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 ng = 0u;       /* origin far from the scene, or a direction the MIX planes */      \
                 oct |= 8u;     /* cannot take: the query in the reference's order (SHADE's redo) */ \
             }                                                                                     \
+            if (INST && kargs()->camFar && depthLeft + 1 == kargs()->max_depth) {                  \
+                /* a far camera: the path starts where its ray enters the world (instEntry) */     \
+                const auto& K_ = *kargs();                                                        \
+                (void)instEntry(K_.S.cx, K_.S.cy, K_.S.cz, K_.S.ext, o, d, inv);                   \
+            }                                                                                     \
         } else if (S.nprims <= 1) {                                                               \
             node = -1;                                                                            \
             if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
@@ -1847,7 +1868,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             if constexpr (WIDE) {
                 // rare: an order-dependent query (or a far origin), repeated in the reference's
                 // order.  Ranks index wshade.
-                const bool redo = wantShade && !needTask && (oct & 8u);
+                const bool redo = !INST && wantShade && !needTask && (oct & 8u);
                 PT_DIAG_ADD(sRedo, (uint32_t)__popcll(__ballot(redo)));
                 if (redo) {
                     const DevScene S2 = ldScene(kargs());
@@ -2147,7 +2168,13 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
         uint32_t oct = woct, inst = 0u;
         // (far origin, or a direction the MIX planes cannot take: the query in the reference's order only)
         const bool far = !INST && (wideFar(S, o) || (PT_WIDE_MIX && mixUnsafe(winv, S.mixLim)));
-        float closest = tmax;
+        // instanced: a far origin moves to the ray's entry into the world (instEntry); distances
+        // are then measured from there and shifted back at the end
+        float3 wo2 = wo;
+        const float shift = (INST && wideFar(S, wo)) ? instEntry(S.cx, S.cy, S.cz, S.ext, wo2, wd, winv) : 0.0f;
+        if (INST) o = wo2;
+        const float tminI = tmin - shift;   // (tmin, tmax of the moved ray: t - shift)
+        float closest = tmax - shift;
         int best = -1, sp = 0;
         bool redo = far;
         float bestLo = -__builtin_inff();
@@ -2163,14 +2190,14 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 else c.tris++;
                 const bool lb = !INST && S.nprims > 1;
                 const uint32_t kh = INST ? inst << S.gBits : 0u;
-                if (S.hasSpheres) wideTest<true>(q, o, d, inv, tmin, closest, best, bestLo, lb, redo, kh);
-                else wideTest<false>(q, o, d, inv, tmin, closest, best, bestLo, lb, redo, kh);
+                if (S.hasSpheres) wideTest<true>(q, o, d, inv, tminI, closest, best, bestLo, lb, redo, kh);
+                else wideTest<false>(q, o, d, inv, tminI, closest, best, bestLo, lb, redo, kh);
             }
             if constexpr (INST) {   // pop; a marker returns to the world ray
                 while ((ng & 0xffu) == 0u && sp > 0) {
                     sp--;
                     ng = my[sp * kWave];
-                    if (ng == kInstMarker) { o = wo; d = wd; inv = winv; oct = woct; ng = 0u; }
+                    if (ng == kInstMarker) { o = wo2; d = wd; inv = winv; oct = woct; ng = 0u; }
                 }
                 if ((ng & 0xffu) == 0u) break;
             } else if ((ng & 0xffu) == 0u) {
@@ -2197,7 +2224,7 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 if (n0.x == 0u) {
                     const float4 r0 = __builtin_bit_cast(float4, n2), r1 = __builtin_bit_cast(float4, n3),
                                  r2 = __builtin_bit_cast(float4, n4);
-                    o = xformPoint(r0, r1, r2, wo);
+                    o = xformPoint(r0, r1, r2, wo2);
                     d = xformDir(r0, r1, r2, wd);
                     inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
                     oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
@@ -2210,7 +2237,7 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 tg = 0u;
                 continue;
             }
-            const uint32_t h = wideHits<!INST && PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tmin, closest);
+            const uint32_t h = wideHits<!INST && PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest);
             ng = (n1.x << 8) | (h >> 24);
             tgBase = n1.y;
             tg = h & 0xffffffu;
@@ -2225,13 +2252,13 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
         hr.mat = -1;
         if (best >= 0) {
             int obj = 0;
-            HitRec x = INST ? makeHitInst(S, (uint32_t)best & kPrimMask, closest, wo, wd, obj)
+            HitRec x = INST ? makeHitInst(S, (uint32_t)best & kPrimMask, closest, wo2, wd, obj)
                             : makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d);
             hr.hit = 1;
             hr.obj = x.obj;
             hr.mat = x.mat;
             hr.front_face = x.front ? 1 : 0;
-            hr.t = closest;
+            hr.t = INST ? closest + shift : closest;
             hr.p[0] = x.p.x; hr.p[1] = x.p.y; hr.p[2] = x.p.z;
             hr.n[0] = x.n.x; hr.n[1] = x.n.y; hr.n[2] = x.n.z;
         }
@@ -2798,6 +2825,8 @@ void writeInstanceRecord(uint32_t id, uint32_t* dst, void* ctx) {
     std::memcpy(dst + 8, (*c.minv)[id].data(), 48);
 }
 
+float mixLimit(double m);   // (below)
+
 int buildInstanced(pt_scene* s) {
     const auto t0 = std::chrono::steady_clock::now();
     const int nm = (int)s->meshFirst.size();
@@ -2808,6 +2837,10 @@ int buildInstanced(pt_scene* s) {
     int64_t gTotal = 0;
     int maxDepthB = 0;
     std::string err;
+    // each mesh's primitive records, boxes and ranks; its tree is built once the instances' reach
+    // into its object space is known (below)
+    std::vector<std::vector<uint32_t>> meshPrims((size_t)nm), meshRank((size_t)nm);
+    std::vector<std::vector<float>> meshBoxes((size_t)nm);
     for (int m = 0; m < nm; m++) {
         const int64_t n = s->meshCount[(size_t)m], first = s->meshFirst[(size_t)m];
         meshG0[(size_t)m] = gTotal;
@@ -2857,9 +2890,9 @@ int buildInstanced(pt_scene* s) {
             sh[11] = (uint32_t)k;
             rank[(size_t)k] = (uint32_t)(gTotal + k);
         }
-        if (n > 0 && !pt::buildWide8(prims.data(), boxes.data(), rank.data(), n, blas[(size_t)m], err))
-            return fail(PT_ERR_STATE, err);
-        maxDepthB = std::max(maxDepthB, blas[(size_t)m].depth);
+        meshPrims[(size_t)m] = std::move(prims);
+        meshBoxes[(size_t)m] = std::move(boxes);
+        meshRank[(size_t)m] = std::move(rank);
         gTotal += n;
     }
     int gBits = 1;
@@ -2874,6 +2907,8 @@ int buildInstanced(pt_scene* s) {
     std::vector<float> iboxes;
     std::vector<uint32_t> used;
     std::vector<float> winst((size_t)std::max<int64_t>(1, ni) * 16, 0.0f);
+    std::vector<std::array<double, 12>> w2o((size_t)ni);   // world-to-object, double
+    double wmn[3] = {INFINITY, INFINITY, INFINITY}, wmx[3] = {-INFINITY, -INFINITY, -INFINITY};   // the world box
     uint32_t objBase = 0;
     for (int64_t i = 0; i < ni; i++) {
         const pt_instance& I = s->inst[(size_t)i];
@@ -2901,6 +2936,8 @@ int buildInstanced(pt_scene* s) {
                 lin = lin && a[r][c] == (r == c ? 1.0 : 0.0);
             }
             minv[(size_t)i][(size_t)(4 * r + 3)] = (float)it;
+            for (int c = 0; c < 3; c++) w2o[(size_t)i][(size_t)(4 * r + c)] = inv[r][c];
+            w2o[(size_t)i][(size_t)(4 * r + 3)] = it;
             id = id && t[r] == 0.0;
         }
         id = id && lin;
@@ -2932,6 +2969,7 @@ int buildInstanced(pt_scene* s) {
                 for (int v = 0; v < 3; v++) grow(o.v[3 * v], o.v[3 * v + 1], o.v[3 * v + 2]);
             }
         }
+        for (int r = 0; r < 3; r++) { wmn[r] = std::min(wmn[r], mn[r]); wmx[r] = std::max(wmx[r], mx[r]); }
         iprims.resize(iprims.size() + pt::kW8PrimDwords, 0u);
         iprims[iprims.size() - pt::kW8PrimDwords + 7] = (uint32_t)i;
         for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)mn[r], -INFINITY));
@@ -2939,6 +2977,42 @@ int buildInstanced(pt_scene* s) {
         used.push_back((uint32_t)i);
     }
     if (used.empty()) return fail(PT_ERR_STATE, "instanced scene: no instance of a non-empty mesh");
+    // The world box (its centre and largest extent: wideFar's region, camFar), and the reach of
+    // world ray origins into each mesh's object space.  Origins within 8 world extents of the
+    // centre (farther camera rays are moved up to the world box first, renderKernelWF<.., INST>)
+    // map into object space within `reach` of the origin; the mesh tree's plane quantum is taken
+    // against that reach, not the mesh's own size, so its outward margin (wideHits) holds for
+    // every ray that enters it.
+    double wext = 0.0, wm = 0.0;
+    for (int a = 0; a < 3; a++) {
+        s->sceneCE[a] = (float)(0.5 * (wmn[a] + wmx[a]));
+        wext = std::max(wext, wmx[a] - wmn[a]);
+        wm = std::max({wm, std::fabs(wmn[a]), std::fabs(wmx[a]), wmx[a] - wmn[a]});
+    }
+    s->sceneCE[3] = std::nextafter((float)wext, INFINITY);
+    s->mixLim = mixLimit(wm);
+    std::vector<double> reach((size_t)nm, 0.0);
+    for (int64_t i = 0; i < ni; i++) {
+        const std::array<double, 12>& W = w2o[(size_t)i];
+        double r = 0.0;
+        for (int c = 0; c < 8; c++) {   // corners of the cube of half-size 8 world extents (+ 1 %)
+            const double h = 8.08 * wext;
+            const double p[3] = {0.5 * (wmn[0] + wmx[0]) + ((c & 1) ? h : -h), 0.5 * (wmn[1] + wmx[1]) + ((c & 2) ? h : -h),
+                                 0.5 * (wmn[2] + wmx[2]) + ((c & 4) ? h : -h)};
+            for (int a = 0; a < 3; a++)
+                r = std::max(r, std::fabs(W[(size_t)(4 * a)] * p[0] + W[(size_t)(4 * a + 1)] * p[1] +
+                                          W[(size_t)(4 * a + 2)] * p[2] + W[(size_t)(4 * a + 3)]));
+        }
+        const int m = s->inst[(size_t)i].mesh;
+        reach[(size_t)m] = std::max(reach[(size_t)m], r);
+    }
+    for (int m = 0; m < nm; m++) {
+        const int64_t n = s->meshCount[(size_t)m];
+        if (n > 0 && !pt::buildWide8(meshPrims[(size_t)m].data(), meshBoxes[(size_t)m].data(), meshRank[(size_t)m].data(),
+                                     n, blas[(size_t)m], err, reach[(size_t)m]))
+            return fail(PT_ERR_STATE, err);
+        maxDepthB = std::max(maxDepthB, blas[(size_t)m].depth);
+    }
     pt::Wide8 top;
     if (!pt::buildWide8Leaf(iprims.data(), iboxes.data(), nullptr, (int64_t)used.size(), 1, top, err))
         return fail(PT_ERR_STATE, err);
@@ -3806,10 +3880,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.seed1 = (uint32_t)(f->seed >> 32);
     P.measureCost = 0;
     {   // wideFar (pt_device.hip) for the camera: its rays then take the reference-order path
-        const float m = std::fmax(std::fmax(std::fabs(cam->origin[0] - s->sceneCE[0]), std::fabs(cam->origin[1] - s->sceneCE[1])),
-                                  std::fabs(cam->origin[2] - s->sceneCE[2]));
-        // (+ the lens: camera ray origins lie within 1.5 lens radii of the camera, per axis)
-        P.camFar = !(m + 1.5f * cam->lens_radius <= 8.0f * s->sceneCE[3]) ? 1 : 0;
+        // (instanced scenes: start at their entry into the world, instEntry).  A lens sample moves
+        // the origin by lens * (x right + y up) with x^2 + y^2 < 1, i.e. by at most
+        // lens * (|right_a| + |up_a|) on axis a, whatever right / up the caller filled in.
+        double m = 0.0;
+        for (int a = 0; a < 3; a++)
+            m = std::max(m, std::fabs((double)cam->origin[a] - (double)s->sceneCE[a]) +
+                                (double)cam->lens_radius * (std::fabs((double)cam->right[a]) + std::fabs((double)cam->up[a])));
+        P.camFar = !(m <= 8.0 * (double)s->sceneCE[3]) ? 1 : 0;
     }
     // Defaults swept on C3 (tools/ab_env.py): sample mode is throughput-bound and prefers full
     // LEAF / SHADE steps.  Compat mode is bound by its slowest pixels' sequential chains: 20 / 12

@@ -501,8 +501,10 @@ int pt_preset_instanced(const char* name, const char* models_dir, int width, int
         out->instances = (pt_instance*)std::malloc(sizeof(pt_instance) * inst.size());
         out->n_materials = (int64_t)flat.materials.size();
         out->materials = (pt_material*)std::malloc(sizeof(pt_material) * std::max<size_t>(1, flat.materials.size()));
-        if (!out->objects || !out->mesh_first || !out->mesh_count || !out->instances || !out->materials)
+        if (!out->objects || !out->mesh_first || !out->mesh_count || !out->instances || !out->materials) {
+            pt_instanced_desc_free(out);   // (what was allocated; the descriptor is left zeroed)
             return fail(PT_ERR_NOMEM, "pt_preset_instanced: out of memory");
+        }
         std::memcpy(out->objects, objs.data(), sizeof(pt_object) * objs.size());
         out->mesh_first[0] = 0;
         out->mesh_count[0] = (int64_t)box.objects.size();

@@ -221,8 +221,8 @@ std::vector<uint32_t> referenceRanks(const uint32_t* leftRef, const uint32_t* ri
 }
 
 bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
-                std::string& err) {
-    return buildWide8Leaf(prims, boxes, rank, n, envLeaf(), out, err);
+                std::string& err, double scaleFloor) {
+    return buildWide8Leaf(prims, boxes, rank, n, envLeaf(), out, err, scaleFloor);
 }
 
 void relocateWide8(Wide8& w, uint32_t nodeBase, uint32_t primBase) {
@@ -276,7 +276,7 @@ bool instanceLeaves(Wide8& top, uint32_t (*instanceOf)(const uint32_t* primRecor
 }
 
 bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, int maxLeaf,
-                    Wide8& out, std::string& err) {
+                    Wide8& out, std::string& err, double scaleFloor) {
     out = Wide8{};
     if (n <= 0) return true;
     if (n >= (int64_t)1 << 26) {
@@ -301,8 +301,10 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
     // Smallest plane quantum: far below any box of interest, far above the rounding of the
     // ray arithmetic (|p - o| * inv: about 2^-21.6 |p - o|, for origins within 8 scene extents of
     // the centre -- farther ones are traced in the reference's order, pt_device.hip wideFar):
-    // 2^-18 of the larger of the scene's extent and coordinates.
-    double ext = 0.0;
+    // 2^-18 of the larger of the scene's extent and coordinates -- or of `scaleFloor` when that is
+    // larger: an instanced mesh's rays arrive in its object space from the whole world
+    // (pt_device.hip buildInstanced), so its planes keep the margin for those origins.
+    double ext = std::isfinite(scaleFloor) && scaleFloor > 0.0 ? scaleFloor : 0.0;
     for (int a = 0; a < 3; a++)
         ext = std::max({ext, std::fabs((double)rootBox.mn[a]), std::fabs((double)rootBox.mx[a]),
                         (double)rootBox.mx[a] - (double)rootBox.mn[a]});

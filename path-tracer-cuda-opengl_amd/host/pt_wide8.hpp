@@ -30,12 +30,15 @@ struct Wide8 {
 // ({v0, rank}...): ties between equal hit distances are decided by it, and it indexes the wide
 // kernels' shading records.  Returns false with `err` set when the tree exceeds the encoding
 // limits.
+// scaleFloor: the plane quantum is at least 2^-18 of max(scaleFloor, the tree's extent and
+// coordinates) -- the distance up to which ray origins keep the boxes' outward margin (instanced
+// meshes: the world's reach in object space).
 bool buildWide8(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, Wide8& out,
-                std::string& err);
+                std::string& err, double scaleFloor = 0.0);
 // buildWide8 with at most maxLeaf (1..3) primitives per leaf child (instancing's top level: one
 // instance per leaf).
 bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* rank, int64_t n, int maxLeaf,
-                    Wide8& out, std::string& err);
+                    Wide8& out, std::string& err, double scaleFloor = 0.0);
 
 // Instancing (two-level tree in one node array).  Record of an instance node, kW8NodeDwords:
 //   [0] 1 if the transform is the identity (the ray is not transformed), [1..2] 0,

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/fetch_calib
 mkdir -p $OUT
 timeout -k 5 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
-for mode in ${MODES:-stream g128 g64s128 g80s128 g80 g80mall g80warm}; do
+for mode in ${MODES:-stream g128 g64s128 g80s128 g80 g80mall g80warm g48}; do
     timeout -k 10 60 tools/micro/fetch_calib $mode > $OUT/$mode.json 2> $OUT/$mode.err || exit $?
     for pass in "fetch:FETCH_SIZE" "ea:TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "hit:TCC_HIT_sum TCC_MISS_sum" \
                 "bub:TCC_BUBBLE_sum TCC_EA0_RDREQ_DRAM_sum"; do
