@@ -1173,6 +1173,9 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #ifndef PT_WIDE_SPEC
 #define PT_WIDE_SPEC 1   // wide kernels: speculative traversal, primitive groups a lane may park while it keeps visiting nodes (0-3)
 #endif
+#ifndef PT_INST_SPEC
+#define PT_INST_SPEC 0   // instanced wide kernels: speculative traversal within an instance's tree (0-1; 1 measured 3 % slower on C5 instanced)
+#endif
 #ifndef PT_WIDE_MIX
 #define PT_WIDE_MIX 1   // wide kernels: plane distances by v_perm + v_fma_mix_f32 (wideHits<MIX>), bit-identical
 #endif
@@ -1244,7 +1247,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Wide kernels, speculative traversal: a lane whose primitive group waits for a LEAF step
     // keeps visiting nodes; the waiting group is parked here ({base, bits} per lane; oct bit 4
     // marks it) and comes back when the current group is empty.
-    constexpr int SPECN = (WIDE && !INST) ? PT_WIDE_SPEC : 0;   // parked groups per lane: a stack, count in oct bits 4-5
+    constexpr int SPECN = WIDE ? (INST ? PT_INST_SPEC : PT_WIDE_SPEC) : 0;   // parked groups per lane: a stack, count in oct bits 4-5
     constexpr bool SPEC = SPECN > 0;
     __shared__ uint32_t pend[SPEC ? 2 * SPECN * kWave : 1];
     // wave-cooperative LEAF steps: the step's queue of (owner lane, primitive) pairs
@@ -1534,8 +1537,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         // binary: room for both children's leaves; wide: a node (the step handles a full queue)
         // or a stack top waiting for queue space (node == -2)
         // binary: room for both children's leaves in the queue; wide: no primitives pending
-        const bool wantNode = WIDE ? ((SPEC ? (tg == 0u || ((oct >> 4) & 3u) < (uint32_t)SPECN) : tg == 0u) &&
-                                      ((ng & 0xffu) != 0u || sp > 0))
+        // (instanced: a lane with primitives waiting visits only siblings of its group -- the same
+        // object space; it pops, and may cross an instance marker, only with none waiting)
+        const bool wantNode = WIDE ? (INST ? ((tg == 0u && ((ng & 0xffu) != 0u || sp > 0)) ||
+                                              (SPEC && tg != 0u && ((oct >> 4) & 3u) < (uint32_t)SPECN && (ng & 0xffu) != 0u))
+                                           : ((SPEC ? (tg == 0u || ((oct >> 4) & 3u) < (uint32_t)SPECN) : tg == 0u) &&
+                                              ((ng & 0xffu) != 0u || sp > 0)))
                                    : (node >= 0 && qn <= LQ - 2);
         const bool wantLeaf = WIDE ? tg != 0u : qn > 0;
         const bool wantShade = (active && (WIDE ? (tg == 0u && (ng & 0xffu) == 0u && sp == 0) : (node == -1 && qn == 0))) ||
@@ -1564,15 +1571,27 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             }
             if constexpr (INST) {
                 if (wantNode) {
+                    if (SPEC && tg != 0u) {   // park the waiting primitive group (a sibling follows: same space)
+                        const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
+                        pend[(2u * c) * kWave + lane] = tgBase;
+                        pend[(2u * c + 1u) * kWave + lane] = tg;
+                        oct += 16u;
+                    }
+                    if constexpr (SPEC) asm volatile("" ::: "memory");
                     // pop to a group with children left; a marker returns the lane to the world
+                    // (oct bit 3: the instance transformed the direction, not only the origin)
                     while ((ng & 0xffu) == 0u && sp > 0) {
                         sp--;
                         ng = my[sp * kWave];
                         if (ng == kInstMarker) {
                             o = f3(wray[0 * kWave + lane], wray[1 * kWave + lane], wray[2 * kWave + lane]);
-                            d = f3(wray[3 * kWave + lane], wray[4 * kWave + lane], wray[5 * kWave + lane]);
-                            inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
-                            oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                            if (oct & 8u) {
+                                d = f3(wray[3 * kWave + lane], wray[4 * kWave + lane], wray[5 * kWave + lane]);
+                                inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                                oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                            } else {
+                                oct &= 7u;
+                            }
                             ng = 0u;
                         }
                     }
@@ -1581,33 +1600,48 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                         const uint32_t child = (ng >> 8) + (bit ^ (oct & 7u));
                         ng &= ~(1u << bit);
                         if (ng & 0xffu) { my[sp * kWave] = ng; sp++; }
-                        const uint32_t off = mul80(child);
-                        const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
-                        const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
-                        const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
-                        const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
-                        const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
-                        if (n0.w == kInstFlag) {   // an instance: into its object space and bottom-level tree
+                        uint32_t off = mul80(child);
+                        uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+                        uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+                        uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+                        uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+                        uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+                        if (n0.w == kInstFlag) {   // an instance: into its object space, and its tree's root in this step
                             wray[0 * kWave + lane] = o.x; wray[1 * kWave + lane] = o.y; wray[2 * kWave + lane] = o.z;
-                            wray[3 * kWave + lane] = d.x; wray[4 * kWave + lane] = d.y; wray[5 * kWave + lane] = d.z;
+                            uint32_t full = 0u;
                             if (n0.x == 0u) {   // (an identity instance keeps the world ray)
                                 const float4 r0 = __builtin_bit_cast(float4, n2), r1 = __builtin_bit_cast(float4, n3),
                                              r2 = __builtin_bit_cast(float4, n4);
-                                o = xformPoint(r0, r1, r2, o);
-                                d = xformDir(r0, r1, r2, d);
-                                inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                                if (n0.y != 0u) {   // translation only: the same origin as xformPoint, the direction kept
+                                    o = f3(o.x + r0.w, o.y + r1.w, o.z + r2.w);
+                                } else {
+                                    wray[3 * kWave + lane] = d.x; wray[4 * kWave + lane] = d.y; wray[5 * kWave + lane] = d.z;
+                                    o = xformPoint(r0, r1, r2, o);
+                                    d = xformDir(r0, r1, r2, d);
+                                    inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                                    full = 8u;
+                                }
                             }
                             const uint32_t oc = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
                             my[sp * kWave] = kInstMarker;   // (depth: host check, wideStackFor)
                             sp++;
-                            ng = (n1.x << 8) | (1u << oc);
-                            oct = oc | (n1.y << 8);   // bits 8+: the instance the lane is in
-                            tg = 0u;
-                        } else {
-                            const uint32_t hits = wideHits(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
-                            ng = (n1.x << 8) | (hits >> 24);
-                            tgBase = n1.y;
-                            tg = hits & 0xffffffu;
+                            oct = oc | full | (n1.y << 8);   // bits 8+: the instance the lane is in
+                            off = mul80(n1.x);               // the mesh tree's root
+                            n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+                            n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+                            n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+                            n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+                            n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+                        }
+                        const uint32_t hits = wideHits(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
+                        ng = (n1.x << 8) | (hits >> 24);
+                        tgBase = n1.y;
+                        tg = hits & 0xffffffu;
+                        if (SPEC && tg == 0u && (oct & 48u)) {   // no new primitives: the last parked group is current again
+                            oct -= 16u;
+                            const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
+                            tgBase = pend[(2u * c) * kWave + lane];
+                            tg = pend[(2u * c + 1u) * kWave + lane];
                         }
                     }
                 }
@@ -2811,14 +2845,15 @@ int buildWideDevice(pt_scene* s, hipStream_t st) {
 int wideStackFor(int depth);
 struct InstRecCtx {
     const std::vector<std::array<float, 12>>* minv;
-    const std::vector<uint8_t>* ident;
+    const std::vector<uint8_t>* ident;   // 1: identity, 2: translation only, 0: general
     const std::vector<pt_instance>* inst;
 };
 uint32_t instanceOfRecord(const uint32_t* rec) { return rec[7]; }
 void writeInstanceRecord(uint32_t id, uint32_t* dst, void* ctx) {
     const InstRecCtx& c = *static_cast<const InstRecCtx*>(ctx);
     std::memset(dst, 0, pt::kW8NodeDwords * 4);
-    dst[0] = (*c.ident)[id] ? 1u : 0u;
+    dst[0] = (*c.ident)[id] == 1 ? 1u : 0u;
+    dst[1] = (*c.ident)[id] == 2 ? 1u : 0u;   // translation only: the kernels move the origin, keep the direction
     dst[3] = pt::kW8InstanceFlag;
     dst[4] = (uint32_t)(*c.inst)[id].mesh;   // (the mesh's root slot once the layout is known)
     dst[5] = id;
@@ -2941,7 +2976,7 @@ int buildInstanced(pt_scene* s) {
             id = id && t[r] == 0.0;
         }
         id = id && lin;
-        ident[(size_t)i] = id ? 1 : 0;
+        ident[(size_t)i] = id ? 1 : (lin ? 2 : 0);
         for (int k = 0; k < 12; k++) winst[(size_t)i * 16 + (size_t)k] = minv[(size_t)i][(size_t)k];
         uint32_t ob = objBase, idf = id ? 1u : lin ? 2u : 0u;   // identity | translation only
         std::memcpy(&winst[(size_t)i * 16 + 12], &ob, 4);

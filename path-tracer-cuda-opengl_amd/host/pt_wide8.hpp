@@ -41,7 +41,8 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
                     Wide8& out, std::string& err, double scaleFloor = 0.0);
 
 // Instancing (two-level tree in one node array).  Record of an instance node, kW8NodeDwords:
-//   [0] 1 if the transform is the identity (the ray is not transformed), [1..2] 0,
+//   [0] 1 if the transform is the identity (the ray is not transformed), [1] 1 if it only
+//   translates (the origin moves, the direction stays), [2] 0,
 //   [3] kW8InstanceFlag (never a valid exponent word: byte 3 of a node's exponents is 0),
 //   [4] the instance's bottom-level root slot, [5] the instance id, [6..7] 0,
 //   [8..19] the world-to-object transform, 3 rows of {m0, m1, m2, t} (fp32).

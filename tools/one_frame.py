@@ -1,4 +1,4 @@
-"""Render one frame (profiling target).  usage: python tools/one_frame.py [c2|c3|c5] [spp] [compat|sample] [chunk]
+"""Render one frame (profiling target).  usage: python tools/one_frame.py [c2|c3|c5|c5i] [spp] [compat|sample] [chunk]
 REPEAT=n renders n frames (later launches use the measured tile costs) and reports the fastest.
 NPARTS=n PART=k render one rank's share of an n-GPU frame (8-row stripes, stripe s on part s % n)."""
 import hashlib
@@ -16,8 +16,12 @@ cfg = os.environ.get("CFG") or (sys.argv[1] if len(sys.argv) > 1 else "c3")
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 rng = ptamd.RNG_SAMPLE if len(sys.argv) > 3 and sys.argv[3] == "sample" else ptamd.RNG_COMPAT
 chunk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
-p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg])
-scene = ptamd.Scene(p.objects, p.materials)
+if cfg == "c5i":   # the instanced bunny field (two-level tree)
+    p = ptamd.InstancedPreset("bunny_field")
+    scene = ptamd.Scene.instanced(p.objects, p.mesh_first, p.mesh_count, p.instances, p.materials)
+else:
+    p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg])
+    scene = ptamd.Scene(p.objects, p.materials)
 film = ptamd.Film(p.width, p.height, 1, stripe_height=8, n_parts=int(os.environ.get("NPARTS", "1")),
                   part=int(os.environ.get("PART", "0")))
 best = None
