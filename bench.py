@@ -241,6 +241,11 @@ def main() -> None:
         else:
             dist.init_process_group(backend)
 
+    if world > 1 and "PT_BUILD_THREADS" not in os.environ:
+        # the ranks of a node share its host cores: each rank's host wide-tree build (before the
+        # timed frames) takes its share of them instead of 16 threads each
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        os.environ["PT_BUILD_THREADS"] = str(max(1, cpu_facts()["usable_cpus"] // max(1, local_world)))
     name, workload = CONFIGS[args.config]
     instanced = args.config in INSTANCED
     if instanced and args.kernel != "wide":

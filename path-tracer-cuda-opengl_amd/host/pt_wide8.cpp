@@ -294,7 +294,10 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
         for (int a = 0; a < 3; a++) B.cen[3 * k + a] = 0.5f * (boxes[6 * k + a] + boxes[6 * k + 3 + a]);
     }
     B.nodes.resize((size_t)(2 * n));
+    // up to 16 host threads; PT_BUILD_THREADS caps them (several ranks on one host share its cores)
     B.maxThreads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char* bt = std::getenv("PT_BUILD_THREADS"))
+        if (std::atoi(bt) > 0) B.maxThreads = std::min(B.maxThreads, std::atoi(bt));
     const int32_t root = B.build(0, (int32_t)n);
     const BBox rootBox = B.nodes[root].box;
 
