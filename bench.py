@@ -66,9 +66,10 @@ STRIPE = 8
 
 def cpu_facts() -> dict:
     """The host the CPU baseline ran on: nproc (os.cpu_count(): every CPU of the machine), the CPUs
-    this process may run on (affinity mask), the cgroup CPU quota if one is set, and the CPU model
-    (/proc/cpuinfo).  On the GPU pool a 1-GPU box is a share of a larger machine: os.cpu_count()
-    counts the whole machine, the share (affinity / quota) is what a process can use."""
+    this process may run on (affinity mask), the cgroup CPU quota if one is set, OMP_NUM_THREADS,
+    and the CPU model (/proc/cpuinfo).  On the GPU pool a 1-GPU box is a share of a larger machine:
+    os.cpu_count() counts the whole machine, the share (affinity / quota / OMP_NUM_THREADS) is what
+    a process may use."""
     nproc = os.cpu_count() or 1
     try:
         allowed = len(os.sched_getaffinity(0))
@@ -91,8 +92,13 @@ def cpu_facts() -> dict:
     except OSError:
         pass
     usable = allowed if quota is None else max(1, min(allowed, int(quota)))
-    return {"nproc": nproc, "cpus_allowed": allowed, "cgroup_cpu_quota": quota, "cpu_model": model,
-            "usable_cpus": usable}
+    # the pool's per-box CPU share (a 1-GPU box gets 16 of its machine's CPUs; OMP_NUM_THREADS
+    # says so there): one thread per CPU of that share
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        usable = min(usable, omp)
+    return {"nproc": nproc, "cpus_allowed": allowed, "cgroup_cpu_quota": quota, "omp_num_threads": omp or None,
+            "cpu_model": model, "usable_cpus": usable}
 
 
 def cpu_baseline(preset, budget_s: float = 12.0, gpu_ref=None) -> dict:
@@ -418,7 +424,9 @@ def main() -> None:
                          "frac": achieved / L2_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS,
-                                 "frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs is not None else None},
+                                 "frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs is not None else None,
+                                 "note": "traffic past L2 (PMC; Infinity-Cache hits included): an upper "
+                                         "bound of the HBM traffic (profiles/r04_fetch_calib)"},
                          "gather_ceiling": {"peak": GATHER_CEILING_GBS, "frac": achieved / GATHER_CEILING_GBS,
                                             "source": "tools/micro/chase.hip, DESIGN.md section 6"},
                          "kernel": "renderKernelWF<STACK, SAMPLE, WIDE=%s>" % ("true" if args.kernel == "wide" else "false"),

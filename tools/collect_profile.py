@@ -53,7 +53,10 @@ def main(tag):
         "traffic_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes": fetch_b, "write_bytes": write_b,
         "source": f"profiles/{tag}/pmc_fetch.csv + pmc_write.csv (separate rocprofv3 --pmc passes; "
-                  "2 x FETCH_SIZE + WRITE_SIZE, KiB -> B)",
+                  "2 x FETCH_SIZE + WRITE_SIZE, KiB -> B; the factor 2 calibrated for this access shape -- "
+                  "random 80-B records at an 80-B stride, one 128-B request per line -- in "
+                  "profiles/r04_fetch_calib/fetch_calib.json; the counters include Infinity-Cache hits, "
+                  "so this is the traffic past L2, an upper bound of the HBM traffic)",
     }
     out["build_id"] = bench["build_id"]
     # TCC (L2) hits and misses of the same launch, when that pass ran: is the tree L2-resident?
