@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cfloat>
 #include <cmath>
@@ -1191,8 +1192,12 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
+#ifndef PT_COMPAT_WIDE_WAVES_PER_EU
+#define PT_COMPAT_WIDE_WAVES_PER_EU PT_WIDE_WAVES_PER_EU   // compat-mode wide kernels (pt_compat.hip)
+#endif
 template <int STACK, bool SAMPLE, bool WIDE>
-constexpr int kWavesPerEU = WIDE ? PT_WIDE_WAVES_PER_EU : kLdsStack<STACK, SAMPLE, WIDE> <= 24
+constexpr int kWavesPerEU = WIDE ? (SAMPLE ? PT_WIDE_WAVES_PER_EU : PT_COMPAT_WIDE_WAVES_PER_EU)
+                                 : kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
                                 : (kLdsStack<STACK, SAMPLE, WIDE> <= 32
                                        ? 5
@@ -3981,7 +3986,18 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         // persistent: exactly the waves that fit at once (the kernel's occupancy per CU, which
         // the LDS stack caps below PT_WAVES_PER_EU per SIMD on deep trees)
         int perCU = 0;
-        if ((rc = persistentWavesPerCU(stack, kernel, perCU, s->instanced))) return rc;
+        {   // (the occupancy of a kernel instantiation does not change: queried once per process)
+            static std::atomic<int> cached[2][2][3];   // [instanced][wide][stack 8, 16, 24]
+            const bool small = stack <= 24 && stack % 8 == 0;
+            std::atomic<int>* c = small ? &cached[s->instanced ? 1 : 0][kernel == PT_KERNEL_WIDE ? 1 : 0][stack / 8 - 1] : nullptr;
+            const int known = c ? c->load(std::memory_order_relaxed) : 0;
+            if (known > 0) {
+                perCU = known;
+            } else {
+                if ((rc = persistentWavesPerCU(stack, kernel, perCU, s->instanced))) return rc;
+                if (c) c->store(perCU, std::memory_order_relaxed);
+            }
+        }
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
         if (std::getenv("PT_ITER_STATS"))
