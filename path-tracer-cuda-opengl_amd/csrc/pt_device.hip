@@ -1192,11 +1192,14 @@ constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK
 #ifndef PT_WIDE_WAVES_PER_EU
 #define PT_WIDE_WAVES_PER_EU 5   // wide tree (96 VGPRs; the stack never limits occupancy): C3 @64 spp 49.7 ms vs 68.8 at 6 (spills), 51.4 at 4
 #endif
+// Compat-mode wide kernels (pt_compat.hip) on shallow trees (STACK 8: C2, C3) at 4 waves per SIMD
+// (104 VGPRs): C3 @1024 spp 806-825 -> 796-798 ms over three runs each, C2 @256 40.0-41.1 ->
+// 41.0-41.4; deeper trees keep 5 (C5 @512: 552-558 at 5, 602-605 at 4).
 #ifndef PT_COMPAT_WIDE_WAVES_PER_EU
-#define PT_COMPAT_WIDE_WAVES_PER_EU PT_WIDE_WAVES_PER_EU   // compat-mode wide kernels (pt_compat.hip)
+#define PT_COMPAT_WIDE_WAVES_PER_EU 4
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
-constexpr int kWavesPerEU = WIDE ? (SAMPLE ? PT_WIDE_WAVES_PER_EU : PT_COMPAT_WIDE_WAVES_PER_EU)
+constexpr int kWavesPerEU = WIDE ? (SAMPLE || STACK > 8 ? PT_WIDE_WAVES_PER_EU : PT_COMPAT_WIDE_WAVES_PER_EU)
                                  : kLdsStack<STACK, SAMPLE, WIDE> <= 24
                                 ? (SAMPLE ? PT_WAVES_PER_EU : 5)
                                 : (kLdsStack<STACK, SAMPLE, WIDE> <= 32
