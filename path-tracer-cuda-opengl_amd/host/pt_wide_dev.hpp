@@ -1,9 +1,10 @@
 // pt_wide_dev.hpp — the compressed 8-wide tree built on the device (csrc/pt_wide_build.hip).
 //
 // Same node and primitive records as the host build (pt_wide8.hpp, layout in pt_wide8.cpp), a
-// different binary tree underneath: instead of the host's binned SAH, parallel locally-ordered
-// clustering (PLOC: clusters in Morton order repeatedly merge with their mutual nearest
-// neighbour within a window, distance = surface area of the merged box), then the same top-down
+// binary tree built in parallel: the host's binned SAH top down (default), or parallel
+// locally-ordered clustering (PT_WIDE_DEVICE_BUILDER=ploc: clusters in Morton order repeatedly
+// merge with their mutual nearest neighbour within a window, distance = surface area of the
+// merged box), then the same top-down
 // collapse to 8 children and the same outward 8-bit quantisation, one level of the wide tree per
 // launch.  Milliseconds instead of the host build's tens of milliseconds to seconds: it is the
 // per-frame rebuild of dynamic scenes (PT_BVH_WIDE_DEVICE).  Closest hits do not depend on the
@@ -64,7 +65,10 @@ private:
         size_t cap = 0;
     };
     hipError_t reserve(Buf& b, size_t bytes);
+    // step 2 by SAH (the root's id left in cid_[0][0])
+    hipError_t buildSah(const WideDevIn& in, hipStream_t stream, float trav, std::string& err);
     Buf pbox_, pchild_, cid_[2], nn_, flag_, pos_, items_[2], cnt_, ofs_, scanTemp_, misc_;
+    Buf sahCen_, sahRef_[2], sahLarge_[2], sahSmall_, sahSplit_, sahBins_, sahMulti_, sahBlk_, sahBlkR_, sahBlkO_, sahCnt_;
 };
 
 }  // namespace pt

@@ -127,7 +127,14 @@ def test_c5_rebuild_per_frame(pt, gpu):
     assert max(times) < 50.0
 
 
-def test_wide_device_rebuild_per_frame(pt, orc, gpu):
+@pytest.fixture(params=["sah", "ploc"])
+def builder(request, monkeypatch):
+    """The device wide tree's binary builder (PT_WIDE_DEVICE_BUILDER)."""
+    monkeypatch.setenv("PT_WIDE_DEVICE_BUILDER", request.param)
+    return request.param
+
+
+def test_wide_device_rebuild_per_frame(pt, orc, gpu, builder):
     """Moving objects rendered with the wide kernel, its tree rebuilt on the device every frame
     (PT_BVH_WIDE_DEVICE): each frame equals the binary kernel's frame of a fresh scene and, for
     compat streams, the oracle's render; the rebuild is deterministic (same stats twice)."""
@@ -157,7 +164,7 @@ def test_wide_device_rebuild_per_frame(pt, orc, gpu):
     np.testing.assert_array_equal(bits(rgb), bits(want))
 
 
-def test_wide_device_identical_objects(pt, orc, gpu):
+def test_wide_device_identical_objects(pt, orc, gpu, builder):
     """5,000 copies of one triangle and 3,000 of one sphere: every clustering distance ties (the
     pairing order must still halve the clusters each pass) and the reference's tie order decides
     every hit."""
@@ -181,7 +188,7 @@ def test_wide_device_identical_objects(pt, orc, gpu):
         np.testing.assert_array_equal(bits(hits[f][h]), bits(ref[f][h]), err_msg=f)
 
 
-def test_c5_wide_device_rebuild(pt, gpu):
+def test_c5_wide_device_rebuild(pt, gpu, builder):
     """1,043,312 triangles: LBVH + device wide tree per frame within a frame budget; the frame
     equals the host-built wide tree's frame."""
     p = pt.Preset("bunny_field", 160, 90)
@@ -194,7 +201,7 @@ def test_c5_wide_device_rebuild(pt, gpu):
         scene.update_objects(objs)
         scene.build_bvh(flags)
         times.append(scene.build_ms)
-    print(f"C5 LBVH + wide device rebuilds {[round(t, 2) for t in times]} ms, wide {scene.wide_info()}")
+    print(f"C5 LBVH + wide device ({builder}) rebuilds {[round(t, 2) for t in times]} ms, wide {scene.wide_info()}")
     assert max(times) < 100.0
     host = pt.Scene(objs, p.materials, device=gpu)
     a, _ = pt.render(scene, pt.Film(160, 90, seed=3), p.camera, 2, p.max_depth, kernel=pt.KERNEL_WIDE, rng=pt.RNG_SAMPLE)

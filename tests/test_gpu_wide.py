@@ -4,8 +4,9 @@ The wide tree visits nodes in its own order (nearest child first) through conser
 8-bit quantised boxes; the closest hit is the minimum of (t, the reference's tie order), which is
 the hit the reference's left-first DFS keeps.  The bar is therefore the same as for the binary
 kernels: every hit record bit-exact, including exact ties (duplicated triangles and spheres).
-Every test runs on both trees: built on the host (binned SAH, at first use) and built on the
-device by pt_scene_build_bvh (PLOC + collapse, PT_BVH_WIDE_DEVICE).
+Every test runs on three trees: built on the host (binned SAH, at first use) and built on the
+device by pt_scene_build_bvh (PT_BVH_WIDE_DEVICE: binned SAH, or PLOC with
+PT_WIDE_DEVICE_BUILDER=ploc, then the collapse).
 """
 import numpy as np
 import pytest
@@ -18,15 +19,19 @@ pytestmark = pytest.mark.gpu
 SCENES = ["triangle_world", "random_world", "test_world", "rtiow", "cornell", "bunny_cornell"]
 
 
-@pytest.fixture(params=["host", "device"])
-def wb(request):
+@pytest.fixture(params=["host", "device", "device_ploc"])
+def wb(request, monkeypatch):
+    if request.param == "device_ploc":
+        monkeypatch.setenv("PT_WIDE_DEVICE_BUILDER", "ploc")
+    else:
+        monkeypatch.delenv("PT_WIDE_DEVICE_BUILDER", raising=False)
     return request.param
 
 
 def make_scene(pt, objs, mats, gpu, wb):
-    flags = pt.PT_BVH_ORIGIN_BOUNDS | (pt.PT_BVH_WIDE_DEVICE if wb == "device" else 0)
+    flags = pt.PT_BVH_ORIGIN_BOUNDS | (pt.PT_BVH_WIDE_DEVICE if wb != "host" else 0)
     s = pt.Scene(objs, mats, device=gpu, flags=flags)
-    if wb == "device" and len(objs):
+    if wb != "host" and len(objs):
         assert s.wide_info()["source"] == 2
     return s
 
@@ -46,7 +51,7 @@ def assert_hits_equal(g, o):
 def trace_both(pt, orc, gpu, wb, objs, mats, rays, tmin=0.001, tmax=np.inf):
     s = make_scene(pt, objs, mats, gpu, wb)
     hits, st = s.trace(rays_to_struct(rays, pt.RAY_DTYPE), tmin, tmax, kernel=pt.KERNEL_WIDE)
-    assert s.wide_info()["source"] == (2 if wb == "device" else 1)
+    assert s.wide_info()["source"] == (2 if wb != "host" else 1)
     ref, rst = orc.trace(objs, orc.build_lbvh(objs, orc.morton_keys(objs), tight=True), rays, tmin, tmax)
     return hits, st, ref, rst
 

@@ -1,7 +1,7 @@
-"""Device-built wide tree (PLOC, PT_BVH_WIDE_DEVICE) vs host-built (binned SAH): build time,
-tree shape, frame time and frame equality.  GPU only.
+"""Device-built wide trees (PT_BVH_WIDE_DEVICE: binned SAH, PLOC) vs host-built (binned SAH):
+build time, tree shape, frame time and frame equality.  GPU only.
 
-    python tools/wide_build_ab.py [c2|c3|c5 ...] [spp]
+    [AB_MODES=host,sah,ploc] python tools/wide_build_ab.py [c2|c3|c5 ...] [spp]
 """
 import os
 import sys
@@ -22,8 +22,9 @@ for cfg in cfgs:
     p = pt.Preset(NAMES[cfg])
     spp = spp_arg[0] if spp_arg else SPP[cfg]
     out = {}
-    for mode in ("host", "device"):
-        flags = pt.PT_BVH_ORIGIN_BOUNDS | (pt.PT_BVH_WIDE_DEVICE if mode == "device" else 0)
+    for mode in os.environ.get("AB_MODES", "host,sah,ploc").split(","):
+        os.environ["PT_WIDE_DEVICE_BUILDER"] = mode
+        flags = pt.PT_BVH_ORIGIN_BOUNDS | (pt.PT_BVH_WIDE_DEVICE if mode != "host" else 0)
         s = pt.Scene(p.objects, p.materials, flags=flags)
         builds = []
         for _ in range(3):
@@ -42,5 +43,6 @@ for cfg in cfgs:
         print(f"{cfg} {mode:6s} lbvh+wide build {min(builds):8.2f} ms wall (device {s.build_ms:7.2f} ms; wide at first use "
               f"{wi['build_ms']:8.2f} ms) depth {wi['depth']} slots {wi['slots']}  frame {best.kernel_ms:8.2f} ms  "
               f"visits {best.node_visits} tris {best.tri_tests} rays {best.rays}", flush=True)
-    same = np.array_equal(out["host"].view(np.uint32), out["device"].view(np.uint32))
+    first = next(iter(out.values()))
+    same = all(np.array_equal(first.view(np.uint32), o.view(np.uint32)) for o in out.values())
     print(f"{cfg} frames identical: {same}", flush=True)
