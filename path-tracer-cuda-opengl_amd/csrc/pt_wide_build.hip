@@ -535,8 +535,9 @@ constexpr int kChunk = 2048;            // primitives per block of a large task 
 constexpr int kPerThread = kChunk / 256;
 constexpr int kBinWords = 16;           // per bin: count, box lo / hi, centroid lo / hi (ordered), pad
 constexpr uint32_t kNoSlot = 0xffffffffu;
-// device counters: nodes allocated, next level's large tasks, wave tasks, error flag, final node count
-enum { kSahNodes = 0, kSahLarge = 1, kSahSmall = 2, kSahErr = 3, kSahTotal = 4, kSahWords = 8 };
+// device counters: nodes allocated, next level's large tasks, wave tasks, error flag, final node
+// count, this level's blocks and tasks of several blocks
+enum { kSahNodes = 0, kSahLarge = 1, kSahSmall = 2, kSahErr = 3, kSahTotal = 4, kSahBlocks = 5, kSahMulti = 6, kSahWords = 8 };
 struct SahTask {                        // 80 B
     uint32_t begin, count, node, firstBlock;
     float lo[3], hi[3], clo[3], chi[3];
@@ -720,9 +721,34 @@ __global__ void sahRootKernel(const uint32_t* __restrict__ rootAcc, int n, float
     }
 }
 
-__global__ void sahZeroBinsKernel(uint32_t* bins, int nbins) {
+// A level's block map on the device: blocks per task (kChunk primitives each) and whether the task
+// needs global bins, an exclusive scan of both, then each task writes its blocks and bin slot.
+__global__ void sahMapCountKernel(const SahTask* __restrict__ tasks, int ntask, uint4* need) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nbins) binInit(bins + (size_t)i * kBinWords);
+    if (i >= ntask) return;
+    const uint32_t c = tasks[i].count;
+    need[i] = make_uint4((c + kChunk - 1) / kChunk, c > (uint32_t)kChunk ? 1u : 0u, 0u, 0u);
+}
+__global__ void sahMapWriteKernel(SahTask* tasks, int ntask, const uint4* __restrict__ need, const uint4* __restrict__ ofs,
+                                  uint2* blockTask, uint32_t* multiTask, uint32_t* cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntask) return;
+    const uint4 nd = need[i], o = ofs[i];
+    SahTask& t = tasks[i];
+    t.firstBlock = o.x;
+    t.binSlot = nd.y ? o.y : kNoSlot;
+    if (nd.y) multiTask[o.y] = (uint32_t)i;
+    for (uint32_t b = 0; b < nd.x; b++) blockTask[o.x + b] = make_uint2((uint32_t)i, t.begin + b * (uint32_t)kChunk);
+    if (i == ntask - 1) {
+        cnt[kSahBlocks] = o.x + nd.x;
+        cnt[kSahMulti] = o.y + nd.y;
+    }
+}
+
+// (grids sized by the host's upper bound; the device counts say how much of them is work)
+__global__ void sahZeroBinsKernel(uint32_t* bins, const uint32_t* __restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (int)cnt[kSahMulti] * 3 * kBins) binInit(bins + (size_t)i * kBinWords);
 }
 
 // One block per (task, chunk of kChunk primitives): LDS bins.  A thread takes kPerThread
@@ -731,9 +757,11 @@ __global__ void sahZeroBinsKernel(uint32_t* bins, int nbins) {
 // one block then picks its split here; a bigger task's bins go to its global bins.
 __global__ __launch_bounds__(256) void sahBinKernel(const SahTask* __restrict__ tasks, const uint2* __restrict__ blockTask,
                                                     const uint32_t* __restrict__ ref, const float4* __restrict__ cen,
-                                                    const float* __restrict__ leafBoxes, uint32_t* bins, SahSplit* splits) {
+                                                    const float* __restrict__ leafBoxes, uint32_t* bins, SahSplit* splits,
+                                                    const uint32_t* __restrict__ cnt) {
     __shared__ uint32_t lb[3 * kBins * kBinWords];
     __shared__ SweepLds sl;
+    if (blockIdx.x >= cnt[kSahBlocks]) return;
     for (int i = threadIdx.x; i < 3 * kBins; i += 256) binInit(lb + i * kBinWords);
     __syncthreads();
     const uint2 bt = blockTask[blockIdx.x];
@@ -811,8 +839,10 @@ __global__ __launch_bounds__(256) void sahBinKernel(const SahTask* __restrict__ 
 
 // one block per task of several blocks (multiTask: task indices): the split from the merged bins
 __global__ __launch_bounds__(128) void sahSplitKernel(const SahTask* __restrict__ tasks, const uint32_t* __restrict__ multiTask,
-                                                      const uint32_t* __restrict__ bins, SahSplit* splits) {
+                                                      const uint32_t* __restrict__ bins, SahSplit* splits,
+                                                      const uint32_t* __restrict__ cnt) {
     __shared__ SweepLds sl;
+    if (blockIdx.x >= cnt[kSahMulti]) return;
     const uint32_t ti = multiTask[blockIdx.x];
     const SahTask& t = tasks[ti];
     sweepSplit(bins + (size_t)t.binSlot * 3 * kBins * kBinWords, t, splits + ti, sl);
@@ -827,8 +857,13 @@ __device__ __forceinline__ bool goesRight(const SahTask& t, const SahSplit& s, u
 
 __global__ __launch_bounds__(256) void sahPartCountKernel(const SahTask* __restrict__ tasks, const SahSplit* __restrict__ splits,
                                                           const uint2* __restrict__ blockTask, const uint32_t* __restrict__ ref,
-                                                          const float4* __restrict__ cen, uint32_t* blockRight) {
+                                                          const float4* __restrict__ cen, uint32_t* blockRight,
+                                                          const uint32_t* __restrict__ cnt) {
     __shared__ uint32_t waveSum[4];
+    if (blockIdx.x >= cnt[kSahBlocks]) {   // no work: a zero in the scan
+        if (threadIdx.x == 0) blockRight[blockIdx.x] = 0u;
+        return;
+    }
     const uint2 bt = blockTask[blockIdx.x];
     const SahTask& t = tasks[bt.x];
     const SahSplit* sp = splits + bt.x;
@@ -845,8 +880,9 @@ __global__ __launch_bounds__(256) void sahPartCountKernel(const SahTask* __restr
 __global__ __launch_bounds__(256) void sahPartScatterKernel(const SahTask* __restrict__ tasks, const SahSplit* __restrict__ splits,
                                                             const uint2* __restrict__ blockTask, const uint32_t* __restrict__ ref,
                                                             const float4* __restrict__ cen, const uint32_t* __restrict__ rightOfs,
-                                                            uint32_t* refOut) {
+                                                            uint32_t* refOut, const uint32_t* __restrict__ cnt) {
     __shared__ uint32_t waveCnt[4];
+    if (blockIdx.x >= cnt[kSahBlocks]) return;
     const uint2 bt = blockTask[blockIdx.x];
     const SahTask& t = tasks[bt.x];
     const SahSplit* sp = splits + bt.x;
@@ -879,7 +915,9 @@ __global__ __launch_bounds__(256) void sahPartScatterKernel(const SahTask* __res
 }
 
 __global__ __launch_bounds__(256) void sahCopyKernel(const SahTask* __restrict__ tasks, const uint2* __restrict__ blockTask,
-                                                     const uint32_t* __restrict__ refOut, uint32_t* ref) {
+                                                     const uint32_t* __restrict__ refOut, uint32_t* ref,
+                                                     const uint32_t* __restrict__ cnt) {
+    if (blockIdx.x >= cnt[kSahBlocks]) return;
     const uint2 bt = blockTask[blockIdx.x];
     const SahTask& t = tasks[bt.x];
     const uint32_t end = min(t.begin + t.count, bt.y + (uint32_t)kChunk);
@@ -1273,9 +1311,8 @@ hipError_t WideDevBuilder::buildSah(const WideDevIn& in, hipStream_t st, float t
     int cur = 0;
     sahRootKernel<<<1, 1, 0, st>>>(rootAcc, (int)n, pbox, static_cast<SahTask*>(sahLarge_[0].p), small, cnt, rootCid);
     WB_TRY(check("root"));
-    std::vector<SahTask> tasks;
-    std::vector<uint2> bmap;
-    std::vector<uint32_t> mlist;
+    uint4* need = static_cast<uint4*>(cnt_.p);
+    uint4* needOfs = static_cast<uint4*>(ofs_.p);
     uint32_t c[kSahWords];
     for (int level = 0;; level++) {
         WB_TRY(hipMemcpyAsync(c, cnt, sizeof(c), hipMemcpyDeviceToHost, st));
@@ -1286,41 +1323,31 @@ hipError_t WideDevBuilder::buildSah(const WideDevIn& in, hipStream_t st, float t
             err = "wide BVH (device): SAH build does not converge";
             return hipErrorUnknown;
         }
-        SahTask* large = static_cast<SahTask*>(sahLarge_[cur].p);
-        tasks.resize(nLarge);
-        WB_TRY(hipMemcpyAsync(tasks.data(), large, nLarge * sizeof(SahTask), hipMemcpyDeviceToHost, st));
-        WB_TRY(hipStreamSynchronize(st));
-        bmap.clear();
-        mlist.clear();
-        for (uint32_t i = 0; i < nLarge; i++) {
-            tasks[i].firstBlock = (uint32_t)bmap.size();
-            tasks[i].binSlot = tasks[i].count > (uint32_t)kChunk ? (uint32_t)mlist.size() : kNoSlot;
-            if (tasks[i].binSlot != kNoSlot) mlist.push_back(i);
-            for (uint32_t b = 0; b < tasks[i].count; b += kChunk) bmap.push_back(make_uint2(i, tasks[i].begin + b));
-        }
-        const unsigned nb = (unsigned)bmap.size(), nMulti = (unsigned)mlist.size();
-        if (nb > blockCap || nMulti > multiCap) {
+        // upper bounds of this level's blocks and multi-block tasks (the exact counts stay on the device)
+        const unsigned nb = (unsigned)(nLarge + nn / kChunk + 1);
+        const unsigned nm = (unsigned)(nLarge < nn / kChunk + 1 ? nLarge : nn / kChunk + 1);
+        if (nb > blockCap || nm > multiCap) {
             err = "wide BVH (device): SAH block map overflow";
             return hipErrorUnknown;
         }
-        WB_TRY(hipMemcpyAsync(large, tasks.data(), nLarge * sizeof(SahTask), hipMemcpyHostToDevice, st));
-        WB_TRY(hipMemcpyAsync(blk, bmap.data(), nb * sizeof(uint2), hipMemcpyHostToDevice, st));
-        if (nMulti) {
-            WB_TRY(hipMemcpyAsync(multi, mlist.data(), nMulti * 4, hipMemcpyHostToDevice, st));
-            const int nbins = (int)nMulti * 3 * kBins;
-            sahZeroBinsKernel<<<blocks(nbins, tb), tb, 0, st>>>(bins, nbins);
-            WB_TRY(check("zero bins"));
-        }
-        sahBinKernel<<<nb, 256, 0, st>>>(large, blk, ref, cen, in.leafBoxes, bins, splits);
+        SahTask* large = static_cast<SahTask*>(sahLarge_[cur].p);
+        sahMapCountKernel<<<blocks(nLarge, tb), tb, 0, st>>>(large, (int)nLarge, need);
+        WB_TRY(check("block counts"));
+        WB_TRY(exclusiveScanU3(scanTemp_.p, need, needOfs, (size_t)nLarge, st));
+        sahMapWriteKernel<<<blocks(nLarge, tb), tb, 0, st>>>(large, (int)nLarge, need, needOfs, blk, multi, cnt);
+        WB_TRY(check("block map"));
+        sahZeroBinsKernel<<<blocks((int64_t)nm * 3 * kBins, tb), tb, 0, st>>>(bins, cnt);
+        WB_TRY(check("zero bins"));
+        sahBinKernel<<<nb, 256, 0, st>>>(large, blk, ref, cen, in.leafBoxes, bins, splits, cnt);
         WB_TRY(check("bins"));
-        if (nMulti) sahSplitKernel<<<nMulti, 128, 0, st>>>(large, multi, bins, splits);
+        sahSplitKernel<<<nm, 128, 0, st>>>(large, multi, bins, splits, cnt);
         WB_TRY(check("split"));
-        sahPartCountKernel<<<nb, 256, 0, st>>>(large, splits, blk, ref, cen, blkR);
+        sahPartCountKernel<<<nb, 256, 0, st>>>(large, splits, blk, ref, cen, blkR, cnt);
         WB_TRY(check("partition count"));
         WB_TRY(exclusiveScanU32(scanTemp_.p, blkR, blkO, (size_t)nb, st));
-        sahPartScatterKernel<<<nb, 256, 0, st>>>(large, splits, blk, ref, cen, blkO, ref2);
+        sahPartScatterKernel<<<nb, 256, 0, st>>>(large, splits, blk, ref, cen, blkO, ref2, cnt);
         WB_TRY(check("partition"));
-        sahCopyKernel<<<nb, 256, 0, st>>>(large, blk, ref2, ref);
+        sahCopyKernel<<<nb, 256, 0, st>>>(large, blk, ref2, ref, cnt);
         WB_TRY(check("copy"));
         WB_TRY(hipMemsetAsync(cnt + kSahLarge, 0, 4, st));
         sahEmitKernel<<<blocks(nLarge, 64), 64, 0, st>>>(large, splits, (int)nLarge, ref, (uint32_t)n, pbox, pchild,
