@@ -149,7 +149,7 @@ int pt_scene_create(int device, const pt_object* objs, int64_t n_objects,
 #define PT_BVH_ORIGIN_BOUNDS 1
 #define PT_BVH_HOST_KEYS 2
 /* PT_BVH_WIDE_DEVICE: also build the wide kernel's compressed 8-wide tree, on the device, in the
- * same call (PLOC clustering + collapse, a few milliseconds even at a million primitives; for
+ * same call (top-down SAH + collapse, a few milliseconds even at a million primitives; for
  * dynamic scenes rebuilt every frame).  Without it PT_KERNEL_WIDE builds the tree at first use on
  * the host (binned SAH, slower to build; PT_WIDE_BUILD=device selects the device build there
  * too; after pt_scene_update_objects the device build is the default).  Either tree gives the
@@ -186,7 +186,7 @@ int pt_scene_bvh_info(pt_scene* scene, int* depth, int64_t* n_nodes, int64_t* de
 /* The wide tree of the current build (0s before its first use): depth (levels), node slots,
  * build time in ms (wall time of the host build + upload, or of the device build when built at
  * first use; 0 when pt_scene_build_bvh built it -- then it is in pt_scene_build_time), source
- * (0 none, 1 host binned SAH, 2 device PLOC). */
+ * (0 none, 1 host SAH, 2 device SAH or PLOC). */
 int pt_scene_wide_info(pt_scene* scene, int* depth, int64_t* node_slots, double* build_ms, int* source);
 /* Download the LBVH in the reference's node layout (2n-1 nodes). */
 int pt_scene_download_bvh(pt_scene* scene, pt_bvh_node* nodes);
