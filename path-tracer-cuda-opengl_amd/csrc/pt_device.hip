@@ -2851,21 +2851,74 @@ int buildWideDevice(pt_scene* s, hipStream_t st) {
 // array: the top level from slot 0, then the meshes' trees.  Shading records in object space, one
 // per mesh primitive (its shading index g); the hit key instance << gBits | g.
 int wideStackFor(int depth);
+// A top-level leaf: an instance entering its mesh's tree at `slot` (the mesh tree's own slot
+// numbering: 0 = its root; relocated with the tree).
+struct InstEntry {
+    uint32_t inst, mesh, slot;
+};
 struct InstRecCtx {
     const std::vector<std::array<float, 12>>* minv;
     const std::vector<uint8_t>* ident;   // 1: identity, 2: translation only, 0: general
-    const std::vector<pt_instance>* inst;
+    const std::vector<InstEntry>* entries;
 };
 uint32_t instanceOfRecord(const uint32_t* rec) { return rec[7]; }
-void writeInstanceRecord(uint32_t id, uint32_t* dst, void* ctx) {
+void writeInstanceRecord(uint32_t e, uint32_t* dst, void* ctx) {
     const InstRecCtx& c = *static_cast<const InstRecCtx*>(ctx);
+    const InstEntry& E = (*c.entries)[e];
     std::memset(dst, 0, pt::kW8NodeDwords * 4);
-    dst[0] = (*c.ident)[id] == 1 ? 1u : 0u;
-    dst[1] = (*c.ident)[id] == 2 ? 1u : 0u;   // translation only: the kernels move the origin, keep the direction
+    dst[0] = (*c.ident)[E.inst] == 1 ? 1u : 0u;
+    dst[1] = (*c.ident)[E.inst] == 2 ? 1u : 0u;   // translation only: the kernels move the origin, keep the direction
     dst[3] = pt::kW8InstanceFlag;
-    dst[4] = (uint32_t)(*c.inst)[id].mesh;   // (the mesh's root slot once the layout is known)
-    dst[5] = id;
-    std::memcpy(dst + 8, (*c.minv)[id].data(), 48);
+    dst[4] = E.slot;   // (+ the mesh tree's base slot once the layout is known)
+    dst[5] = E.inst;
+    dst[6] = E.mesh;   // (layout only; cleared with the relocation)
+    std::memcpy(dst + 8, (*c.minv)[E.inst].data(), 48);
+}
+
+// Partial re-braiding (Benthin et al. 2017): an instance enters its mesh tree below the root, one
+// top-level leaf per internal child of the mesh root, each with its own world box, so the top
+// level separates overlapping instances at the mesh's second level.  The child boxes come from the
+// root's quantised planes (outward-rounded: they contain the subtrees).  Returns the mesh root's
+// internal children {slot, object-space box}; empty when the root has leaf children (then the
+// instance enters at the root).
+struct SubRoot {
+    uint32_t slot;
+    double box[6];
+};
+std::vector<SubRoot> nodeChildren(const pt::Wide8& w, uint32_t slot) {
+    std::vector<SubRoot> out;
+    if (w.nodes.size() < (size_t)(slot + 1) * pt::kW8NodeDwords) return out;
+    const uint32_t* R = w.nodes.data() + (size_t)slot * pt::kW8NodeDwords;
+    float p[3];
+    std::memcpy(p, R, 12);
+    for (int j = 0; j < 8; j++) {
+        const uint32_t mb = (R[6 + (j >> 2)] >> (8 * (j & 3))) & 0xffu;
+        if (mb == 0u) continue;
+        if ((mb & 0xf8u) != 0x38u) return {};   // a leaf child at the root
+        SubRoot sr;
+        sr.slot = R[4] + (mb & 7u);
+        for (int a = 0; a < 3; a++) {
+            const int e = (int)((R[3] >> (8 * a)) & 0xffu) - 127;
+            const uint32_t ql = (R[8 + 4 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu;
+            const uint32_t qh = (R[10 + 4 * a + (j >> 2)] >> (8 * (j & 3))) & 0xffu;
+            sr.box[a] = (double)p[a] + std::ldexp((double)ql, e);
+            sr.box[3 + a] = (double)p[a] + std::ldexp((double)qh, e);
+        }
+        out.push_back(sr);
+    }
+    return out;
+}
+// The entries `levels` wide levels below the root (a node with leaf children stays an entry).
+void meshSubRoots(const pt::Wide8& w, uint32_t slot, const double* box, int levels, std::vector<SubRoot>& out) {
+    std::vector<SubRoot> ch = levels > 0 ? nodeChildren(w, slot) : std::vector<SubRoot>{};
+    if (ch.empty()) {
+        SubRoot sr;
+        sr.slot = slot;
+        for (int k = 0; k < 6; k++) sr.box[k] = box[k];
+        out.push_back(sr);
+        return;
+    }
+    for (const SubRoot& c : ch) meshSubRoots(w, c.slot, c.box, levels - 1, out);
 }
 
 float mixLimit(double m);   // (below)
@@ -2946,8 +2999,7 @@ int buildInstanced(pt_scene* s) {
     // instances: world-to-object transforms, world boxes (every mesh vertex transformed, in double)
     std::vector<std::array<float, 12>> minv((size_t)ni);
     std::vector<uint8_t> ident((size_t)ni, 0);
-    std::vector<uint32_t> iprims;
-    std::vector<float> iboxes;
+    std::vector<std::array<double, 6>> ibox((size_t)ni);   // world box of each instance
     std::vector<uint32_t> used;
     std::vector<float> winst((size_t)std::max<int64_t>(1, ni) * 16, 0.0f);
     std::vector<std::array<double, 12>> w2o((size_t)ni);   // world-to-object, double
@@ -3013,10 +3065,10 @@ int buildInstanced(pt_scene* s) {
             }
         }
         for (int r = 0; r < 3; r++) { wmn[r] = std::min(wmn[r], mn[r]); wmx[r] = std::max(wmx[r], mx[r]); }
-        iprims.resize(iprims.size() + pt::kW8PrimDwords, 0u);
-        iprims[iprims.size() - pt::kW8PrimDwords + 7] = (uint32_t)i;
-        for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)mn[r], -INFINITY));
-        for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)mx[r], INFINITY));
+        for (int r = 0; r < 3; r++) {
+            ibox[(size_t)i][(size_t)r] = mn[r];
+            ibox[(size_t)i][(size_t)(3 + r)] = mx[r];
+        }
         used.push_back((uint32_t)i);
     }
     if (used.empty()) return fail(PT_ERR_STATE, "instanced scene: no instance of a non-empty mesh");
@@ -3056,10 +3108,57 @@ int buildInstanced(pt_scene* s) {
             return fail(PT_ERR_STATE, err);
         maxDepthB = std::max(maxDepthB, blas[(size_t)m].depth);
     }
+    // top-level leaves: per instance, its mesh root's internal children (re-braided; PT_INST_REBRAID=0:
+    // the mesh root), each with the world box of its object-space box (8 corners in double)
+    const char* rbv = std::getenv("PT_INST_REBRAID");
+    const int rebraid = rbv ? std::max(0, std::min(3, std::atoi(rbv))) : 1;
+    std::vector<std::vector<SubRoot>> sub((size_t)nm);
+    for (int m = 0; m < nm; m++) {
+        const double inf[6] = {-INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, INFINITY};
+        if (rebraid > 0) meshSubRoots(blas[(size_t)m], 0u, inf, rebraid, sub[(size_t)m]);
+        if (sub[(size_t)m].size() == 1) sub[(size_t)m].clear();   // (the root itself)
+    }
+    std::vector<InstEntry> entries;
+    std::vector<uint32_t> iprims;
+    std::vector<float> iboxes;
+    auto addEntry = [&](uint32_t i, uint32_t mesh, uint32_t slot, const double* b) {
+        iprims.resize(iprims.size() + pt::kW8PrimDwords, 0u);
+        iprims[iprims.size() - pt::kW8PrimDwords + 7] = (uint32_t)entries.size();
+        for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)b[r], -INFINITY));
+        for (int r = 0; r < 3; r++) iboxes.push_back(std::nextafter((float)b[3 + r], INFINITY));
+        entries.push_back({i, mesh, slot});
+    };
+    for (uint32_t i : used) {
+        const pt_instance& I = s->inst[(size_t)i];
+        const std::vector<SubRoot>& sr = sub[(size_t)I.mesh];
+        if (sr.empty()) {
+            addEntry(i, (uint32_t)I.mesh, 0u, ibox[(size_t)i].data());
+            continue;
+        }
+        for (const SubRoot& r : sr) {
+            double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int c = 0; c < 8; c++) {
+                const double q[3] = {r.box[(c & 1) ? 3 : 0], r.box[(c & 2) ? 4 : 1], r.box[(c & 4) ? 5 : 2]};
+                for (int a = 0; a < 3; a++) {
+                    const double w = (double)I.m[4 * a] * q[0] + (double)I.m[4 * a + 1] * q[1] + (double)I.m[4 * a + 2] * q[2] +
+                                     (double)I.m[4 * a + 3];
+                    mn[a] = std::min(mn[a], w);
+                    mx[a] = std::max(mx[a], w);
+                }
+            }
+            // (never beyond the instance's exact box)
+            double b[6];
+            for (int a = 0; a < 3; a++) {
+                b[a] = std::max(mn[a], ibox[(size_t)i][(size_t)a]);
+                b[3 + a] = std::min(mx[a], ibox[(size_t)i][(size_t)(3 + a)]);
+            }
+            addEntry(i, (uint32_t)I.mesh, r.slot, b);
+        }
+    }
     pt::Wide8 top;
-    if (!pt::buildWide8Leaf(iprims.data(), iboxes.data(), nullptr, (int64_t)used.size(), 1, top, err))
+    if (!pt::buildWide8Leaf(iprims.data(), iboxes.data(), nullptr, (int64_t)entries.size(), 1, top, err))
         return fail(PT_ERR_STATE, err);
-    InstRecCtx ctx{&minv, &ident, &s->inst};
+    InstRecCtx ctx{&minv, &ident, &entries};
     if (!pt::instanceLeaves(top, instanceOfRecord, writeInstanceRecord, &ctx, err)) return fail(PT_ERR_STATE, err);
     // layout: the top level from slot 0, then each mesh's tree (child and primitive bases relocated)
     const uint32_t topSlots = (uint32_t)(top.nodes.size() / pt::kW8NodeDwords);
@@ -3073,7 +3172,10 @@ int buildInstanced(pt_scene* s) {
     }
     if ((int64_t)nodeBase >= ((int64_t)1 << 24)) return fail(PT_ERR_STATE, "instanced BVH: more than 2^24 node slots");
     for (size_t k = 0; k < top.nodes.size(); k += pt::kW8NodeDwords)
-        if (top.nodes[k + 3] == pt::kW8InstanceFlag) top.nodes[k + 4] = meshRoot[top.nodes[k + 4]];
+        if (top.nodes[k + 3] == pt::kW8InstanceFlag) {
+            top.nodes[k + 4] += meshRoot[top.nodes[k + 6]];
+            top.nodes[k + 6] = 0u;
+        }
     std::vector<uint32_t> nodes = top.nodes, prims;
     for (int m = 0; m < nm; m++) {
         nodes.insert(nodes.end(), blas[(size_t)m].nodes.begin(), blas[(size_t)m].nodes.end());
