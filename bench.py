@@ -241,7 +241,10 @@ def main() -> None:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # PT_DIST_FORCE=1: the multi-rank path (process group, gather, barriers, reductions) even for
+    # one rank -- a one-GPU box can run the RCCL gather of a real frame (never a reported number)
+    dist_on = world > 1 or os.environ.get("PT_DIST_FORCE") == "1"
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -275,7 +278,7 @@ def main() -> None:
     out_format = ptamd.OUT_RGBA8 if rgba8 else ptamd.OUT_RGB32F
     local_buf = torch.zeros((max_rows * w * chans,), dtype=tdt, device=dev)
     ref_buf = torch.zeros_like(local_buf)   # the reference-order kernel's frame (warmup step 1)
-    gathered = torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if world > 1 and rank == 0 else None
+    gathered = torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if dist_on and rank == 0 else None
     stream = torch.cuda.current_stream(dev)
 
     sample = args.rng == "sample"
@@ -291,7 +294,7 @@ def main() -> None:
                              stream=stream.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
                              shade_batch=args.shade_batch, rng=ptamd.RNG_SAMPLE if sample else ptamd.RNG_COMPAT,
                              chunk=args.chunk, out_format=out_format)
-        if world > 1:   # the frame's stripes to rank 0 (one gather; SURVEY 8(e) ncclGather)
+        if dist_on:   # the frame's stripes to rank 0 (one gather; SURVEY 8(e) ncclGather)
             if backend == "nccl":
                 ptdist.gather_to_root(local_buf, world, rank, gathered)
             else:
@@ -320,7 +323,7 @@ def main() -> None:
         check(frame())
     if args.kernel == "wide" and not instanced:   # built at the first wide render (host binned SAH)
         scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -337,12 +340,12 @@ def main() -> None:
         spec_visits += st.node_visits
         kms += st.kernel_ms
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
     t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
+    if dist_on:
         mx = t[:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t[1:].clone()
@@ -370,7 +373,7 @@ def main() -> None:
                           "oracle/), one frame after one warmup"}
 
     if rank == 0:
-        if world > 1:   # un-permute the stripes of the last frame (rank 0 holds the full image)
+        if dist_on:   # un-permute the stripes of the last frame (rank 0 holds the full image)
             img = ptdist.assemble(gathered, h, w, STRIPE, world, chans)
             torch.cuda.synchronize(dev)
         else:
@@ -469,7 +472,7 @@ def main() -> None:
                         "nodes (wide kernel); CPU at 1 spp (bounded sample), GPU over the whole frame"}
             out["cpu_baseline"] = cpu_baseline(ptamd.Preset(name) if instanced else preset, gpu_ref=gpu_ref)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

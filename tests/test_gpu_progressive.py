@@ -200,6 +200,33 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     np.testing.assert_array_equal(read_png(one), read_png(two))
 
 
+def test_bench_rccl_gather_one_rank(tmp_path):
+    """bench.py's multi-rank flow over RCCL (backend "nccl": process group, dist.gather of the
+    RGBA8 stripes, barriers, max / sum reductions) with the one rank a one-GPU box allows
+    (PT_DIST_FORCE=1): the PNG equals the plain 1-rank PNG and the reported rays are the frame's."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from helpers import read_png
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--config", "c2", "--spp", "4", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+              "--no-compat", "--no-interactive"]
+    one, forced = str(tmp_path / "one.png"), str(tmp_path / "rccl.png")
+    r1 = subprocess.run([sys.executable] + common + ["--png", one], cwd=repo, capture_output=True, text=True,
+                        timeout=300)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    env = dict(os.environ, PT_DIST_FORCE="1", PT_DIST_BACKEND="nccl")
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                         "--master-addr", "127.0.0.1", "--master-port", "29519"] + common[:1] + ["--gpus", "1"] +
+                        common[1:] + ["--png", forced], cwd=repo, capture_output=True, text=True, timeout=300, env=env)
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    np.testing.assert_array_equal(read_png(one), read_png(forced))
+    a = json.loads(r1.stdout.strip().splitlines()[-1])
+    b = json.loads(r2.stdout.strip().splitlines()[-1])
+    assert a["config"]["rays_per_frame"] == b["config"]["rays_per_frame"] > 0
+
+
 def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     """C4 (BASELINE.json configs[3]: the C3 scene at 1920x1080, 4096 spp, row-tiled over 8 GPUs)
     through bench.py's own multi-rank flow: 8 ranks over gloo sharing this one GPU (a rehearsal,
