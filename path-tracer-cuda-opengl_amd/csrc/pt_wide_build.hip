@@ -19,7 +19,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <vector>
 
 #include "pt_prims.hpp"
 #include "pt_wide_dev.hpp"
