@@ -186,6 +186,29 @@ def test_wide_large_soup_trace_and_render(pt, orc, gpu, wb):
     np.testing.assert_array_equal(bits(frames[1]), bits(frames[0]))
 
 
+@pytest.mark.parametrize("name", ["bunny_cornell", "cornell"])
+def test_device_sah_tree_quality(pt, gpu, monkeypatch, name):
+    """The device's top-down SAH tree (PT_WIDE_DEVICE_BUILDER=sah) traverses like the host SAH
+    tree: over the same rays its wide-node visits and primitive tests stay within 10 % of the
+    host tree's (a wrong scan or sweep would still give valid trees and identical hits, only
+    slower ones -- PLOC's tree, for scale, visits 7-10 % more nodes on these scenes)."""
+    p = pt.Preset(name, 160, 90)
+    rays = rays_to_struct(random_rays(20000, seed=91, objects=p.objects), pt.RAY_DTYPE)
+    stats = {}
+    for wb in ("host", "sah"):
+        monkeypatch.setenv("PT_WIDE_DEVICE_BUILDER", "sah")
+        flags = pt.PT_BVH_ORIGIN_BOUNDS | (pt.PT_BVH_WIDE_DEVICE if wb == "sah" else 0)
+        s = pt.Scene(p.objects, p.materials, device=gpu, flags=flags)
+        _, st = s.trace(rays, 0.001, np.inf, kernel=pt.KERNEL_WIDE)
+        assert s.wide_info()["source"] == (2 if wb == "sah" else 1)
+        stats[wb] = st
+    h, d = stats["host"], stats["sah"]
+    print(f"{name}: host visits {h.node_visits} tests {h.tri_tests + h.sphere_tests}; "
+          f"device SAH visits {d.node_visits} tests {d.tri_tests + d.sphere_tests}")
+    assert d.node_visits <= 1.10 * h.node_visits
+    assert d.tri_tests + d.sphere_tests <= 1.10 * (h.tri_tests + h.sphere_tests)
+
+
 def edge_scene(kind):
     """Scenes at the edges of the wide tree's encoding: tiny and huge coordinates (the plane
     quantum is relative to the scene extent), degenerate triangles, everything at one point, a
