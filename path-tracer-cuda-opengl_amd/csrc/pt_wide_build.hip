@@ -4,7 +4,8 @@
 //    would test the LBVH's leaves (the tie order of the closest hit), from the leaf up: at each
 //    ancestor, the offset of the child's part in its parent's visit (leaf children first, left
 //    then right; then the right subtree; then the left one).  = pt::referenceRanks, in parallel.
-// 2. Binary tree: PLOC over the leaves in Morton order.  Each pass: every cluster finds its
+// 2. Binary tree: top-down SAH (default; "binned SAH" below), or with PT_WIDE_DEVICE_BUILDER=ploc
+//    PLOC over the leaves in Morton order.  PLOC pass: every cluster finds its
 //    nearest neighbour within kRadius positions (smallest merged surface area; ties by the pair's
 //    positions, a strict total order, so the globally closest pair is mutual and every pass
 //    merges), mutual pairs merge into a new node at the lower position, survivors are compacted.
@@ -13,7 +14,7 @@
 // 3. Collapse + quantisation, one wide level per launch pair: count (children, primitives, child
 //    block), exclusive scan, write.  Slots and primitive records are allocated in level order,
 //    parents' order, slot order -- the host build's breadth-first order -- so the output is
-//    deterministic (the node ids PLOC hands out by atomic counter never reach it).
+//    deterministic (the node ids either builder hands out never reach it).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
