@@ -518,7 +518,7 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
 
 // ---------------------------------------------------------------------------------- binned SAH
 // Step 2 by top-down SAH instead of PLOC (PT_WIDE_DEVICE_BUILDER=sah, the default): the host
-// build's rule (pt_wide8.cpp: 32 centroid bins per axis, the split minimising count x area summed
+// build's rule (pt_wide8.cpp: centroid bins per axis -- 32 here, 64 there --, the split minimising count x area summed
 // over the two sides, subtrees of at most 3 primitives kept as one leaf group when that is
 // cheaper) run on the device.  Tasks -- a node and its primitives, contiguous in `ref` -- of more
 // than kWaveTask primitives are split level by level: one block per kChunk primitives bins its part
