@@ -56,12 +56,7 @@ struct BNode {
     int32_t first = 0, count = 0;    // leaf: idx[first, first + count)
 };
 
-// Centroid bins per axis (round 4: 64; at the bench configs C5 443.3 -> 441.3 ms, C3 equal, 128 bins
-// no better: tools/ab_libs_bench.sh)
-#ifndef PT_HOST_BINS
-#define PT_HOST_BINS 64
-#endif
-constexpr int kBins = PT_HOST_BINS;
+constexpr int kBins = 32;
 constexpr double kPrimCost = 1.0;
 
 // Build parameters (tuning knobs, PT_WIDE_MAX_LEAF / PT_WIDE_TRAV_COST): at most kMaxLeaf <= 3
