@@ -30,7 +30,10 @@ instructions) come from the committed profiles of the SAME libpt.so build (`buil
 else null.  `cpu_baseline` = the CPU restatement (oracle/) on the host cores, rank 0 at N = 1 only,
 on a bounded sample.  `interactive` (N = 1) = frames/s of the progressive interactive mode at
 1 / 4 / 16 spp.  Every timed frame is compared with the reference-order kernel's frame (pixels
-and rays).
+and rays).  With N > 1 consecutive steps alternate between two films on two streams (two frames
+in flight: a frame's first waves overlap the previous frame's tail, which is 7 % of a 1/8 share);
+`ms_per_step` is then the wall time per frame of the sequence, and the roofline's launch duration
+is taken from a warmup launch that ran alone.
 """
 import argparse
 import json
@@ -177,27 +180,36 @@ def interactive(scene, preset, dev, stream, local, frames=(30, 20, 10), spps=(1,
     (pt_film_clear), `spp` samples accumulated and converted to RGBA8 on the device
     (PT_OUT_RGBA8_SURFACE).  Frames are enqueued without host synchronisation (pt_render_ex
     without pt_stats); frames/s = frames / wall time from the first enqueue to the last frame
-    done."""
+    done.  `fps_2_streams`: the same frames alternating between two films (double-buffered
+    surfaces) on two streams, so that a frame's first waves start while the previous frame's
+    last paths finish (throughput; each frame's latency stays `ms_per_frame`)."""
     w, h = preset.width, preset.height
-    film = ptamd.Film(w, h, 1, device=local)
-    buf = torch.empty((w * h * 4,), dtype=torch.uint8, device=dev)
+    films = [ptamd.Film(w, h, 1, device=local), ptamd.Film(w, h, 1, device=local)]
+    bufs = [torch.empty((w * h * 4,), dtype=torch.uint8, device=dev) for _ in range(2)]
+    streams = [stream, torch.cuda.Stream(dev)]
     cam = ptamd.Camera.from_buffer_copy(bytes(preset.camera))
     out = {}
     for spp, n in zip(spps, frames):
-        for it in range(2):   # warm (tile order, allocations), then timed
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            for k in range(n):
-                ptamd.camera_move(cam, (0, 2, 1, 3)[k % 4], 0.01)   # forward, left, back, right
-                film.clear(stream.cuda_stream)
-                ptamd.render(scene, film, cam, spp, preset.max_depth, out=buf.data_ptr(), stream=stream.cuda_stream,
-                             rng=ptamd.RNG_SAMPLE, accumulate=True, out_format=ptamd.OUT_RGBA8_SURFACE, wait=False)
-            torch.cuda.synchronize(dev)
-            el = time.perf_counter() - t0
-        st = film.stats()
-        out[f"{spp}spp"] = {"fps": n / el, "ms_per_frame": el / n * 1e3, "frames": n,
-                            "rays_per_frame": st.rays, "kernel_ms": st.kernel_ms}
-    film.close()
+        res = {}
+        for pipes in (1, 2):
+            for it in range(2):   # warm (tile order, allocations), then timed
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for k in range(n):
+                    j = k % pipes
+                    ptamd.camera_move(cam, (0, 2, 1, 3)[k % 4], 0.01)   # forward, left, back, right
+                    films[j].clear(streams[j].cuda_stream)
+                    ptamd.render(scene, films[j], cam, spp, preset.max_depth, out=bufs[j].data_ptr(),
+                                 stream=streams[j].cuda_stream, rng=ptamd.RNG_SAMPLE, accumulate=True,
+                                 out_format=ptamd.OUT_RGBA8_SURFACE, wait=False)
+                torch.cuda.synchronize(dev)
+                res[pipes] = time.perf_counter() - t0
+            if pipes == 1:
+                st = films[0].stats()   # (the sequential frames' counters and kernel time)
+        out[f"{spp}spp"] = {"fps": n / res[1], "ms_per_frame": res[1] / n * 1e3, "frames": n,
+                            "rays_per_frame": st.rays, "kernel_ms": st.kernel_ms, "fps_2_streams": n / res[2]}
+    for f in films:
+        f.close()
     return out
 
 
@@ -224,6 +236,8 @@ def main() -> None:
                     help="frame format rendered and gathered: rgba8 (default: quantised on the device like "
                          "PngImage::saveColor, 4 B/pixel on the wire) or f32 (linear-sqrt RGB, 12 B/pixel)")
     ap.add_argument("--png", default="", help="rank 0 writes the last (assembled) frame to this PNG")
+    ap.add_argument("--frames-in-flight", type=int, default=0, choices=[0, 1, 2],
+                    help="frames rendered concurrently on two streams (0 = 2 for N > 1, 1 for N = 1)")
     ap.add_argument("--kernel", default="wide", choices=["wide", "wavefront"],
                     help="wide (default): the compressed 8-wide SAH tree, nearest child first; wavefront: the "
                          "binary LBVH in the reference's visiting order.  Same image either way")
@@ -271,36 +285,46 @@ def main() -> None:
         scene = ptamd.Scene(preset.objects, preset.materials, device=local)
         scene.build_bvh()   # again: the first build in a process also pays one-time module loading
         scene_build = {"lbvh_device_ms": scene.build_ms}
-    film = ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank)
+    # Frames in flight (N > 1; --frames-in-flight): consecutive steps alternate between two films
+    # (and output buffers) on two streams, so a frame's first waves start while the previous
+    # frame's last paths finish -- the launch's tail, 7 % of a 1/8 share of C3 but 0.2 % of the
+    # whole frame (tools/pipe_frames.py), so N = 1 renders one frame at a time.  Every frame is
+    # still rendered in full and checked against the reference-order frame.
+    films = [ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank) for _ in range(2)]
     max_rows = ptdist.max_rows(h, STRIPE, world)
     rgba8 = args.output == "rgba8"
     chans, tdt = (4, torch.uint8) if rgba8 else (3, torch.float32)
     out_format = ptamd.OUT_RGBA8 if rgba8 else ptamd.OUT_RGB32F
-    local_buf = torch.zeros((max_rows * w * chans,), dtype=tdt, device=dev)
-    ref_buf = torch.zeros_like(local_buf)   # the reference-order kernel's frame (warmup step 1)
-    gathered = torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if dist_on and rank == 0 else None
-    stream = torch.cuda.current_stream(dev)
+    local_bufs = [torch.zeros((max_rows * w * chans,), dtype=tdt, device=dev) for _ in range(2)]
+    ref_buf = torch.zeros_like(local_bufs[0])   # the reference-order kernel's frame (warmup step 1)
+    gathered = [torch.empty((world * max_rows * w * chans,), dtype=tdt, device=dev) if dist_on and rank == 0 else None
+                for _ in range(2)]
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    film, local_buf, stream = films[0], local_bufs[0], streams[0]   # (single-frame uses below)
 
     sample = args.rng == "sample"
 
     kernel_id = ptamd.KERNEL_WIDE if args.kernel == "wide" else ptamd.KERNEL_WAVEFRONT
 
-    def frame(kernel=kernel_id):
+    def frame(j, kernel=kernel_id, wait=False):
         # every step renders the SAME frame: streams back to curand_init(seed, pixel, 0)
-        # (sample mode is stateless: a pure function of seed, pixel and sample)
+        # (sample mode is stateless: a pure function of seed, pixel and sample).  Film j, its
+        # buffer and stream; wait=False enqueues it (films[j].stats() waits for it).
+        f, buf, s = films[j], local_bufs[j], streams[j]
         if not sample:
-            film.reset(stream.cuda_stream)
-        _, st = ptamd.render(scene, film, preset.camera, spp, depth, out=local_buf.data_ptr(),
-                             stream=stream.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
+            f.reset(s.cuda_stream)
+        _, st = ptamd.render(scene, f, preset.camera, spp, depth, out=buf.data_ptr(),
+                             stream=s.cuda_stream, kernel=kernel, leaf_batch=args.leaf_batch,
                              shade_batch=args.shade_batch, rng=ptamd.RNG_SAMPLE if sample else ptamd.RNG_COMPAT,
-                             chunk=args.chunk, out_format=out_format)
-        if dist_on:   # the frame's stripes to rank 0 (one gather; SURVEY 8(e) ncclGather)
-            if backend == "nccl":
-                ptdist.gather_to_root(local_buf, world, rank, gathered)
-            else:
-                g = ptdist.gather_to_root(local_buf.cpu(), world, rank)
-                if rank == 0:
-                    gathered.copy_(g)
+                             chunk=args.chunk, out_format=out_format, wait=wait)
+        if dist_on:   # the frame's stripes to rank 0 (one gather; SURVEY 8(e) ncclGather), after it on its stream
+            with torch.cuda.stream(s):
+                if backend == "nccl":
+                    ptdist.gather_to_root(buf, world, rank, gathered[j])
+                else:
+                    g = ptdist.gather_to_root(buf.cpu(), world, rank)
+                    if rank == 0:
+                        gathered[j].copy_(g)
         return st
 
     # Warmup 1 uses the ray-synchronous kernel, whose traversal follows the reference's node
@@ -308,19 +332,34 @@ def main() -> None:
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
     # (An instanced scene has only the wide kernel: its first frame is the one later frames equal.)
-    ref_st = frame(ptamd.KERNEL_WIDE if instanced else ptamd.KERNEL_SIMPLE)
-    ref_buf.copy_(local_buf)
+    ref_st = frame(0, ptamd.KERNEL_WIDE if instanced else ptamd.KERNEL_SIMPLE, wait=True)
+    ref_buf.copy_(local_bufs[0])
 
-    def check(st):
+    def check(st, j):
         # every frame: this rank's pixels and ray count equal the reference-order frame's
-        if st.rays != ref_st.rays or not torch.equal(local_buf, ref_buf) or (
+        with torch.cuda.stream(streams[j]):
+            same = torch.equal(local_bufs[j], ref_buf)
+        if st.rays != ref_st.rays or not same or (
                 args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
                                                 st.sphere_tests != ref_st.sphere_tests)):
             raise SystemExit("frame differs from the reference-order frame")
 
-    check(ref_st)   # (also loads torch's comparison kernels before the timed region)
-    for _ in range(max(0, args.warmup - 1)):
-        check(frame())
+    def finish(j):
+        st = films[j].stats()   # (waits for film j's frame)
+        check(st, j)
+        return st
+
+    check(ref_st, 0)   # (also loads torch's comparison kernels before the timed region)
+    fif = args.frames_in_flight or (2 if world > 1 else 1)
+    warm_kms = ref_st.kernel_ms
+    if fif == 2:
+        st1 = frame(1, wait=True)   # (film 1's first launch: its tile costs for the launch order)
+        check(st1, 1)
+        warm_kms = st1.kernel_ms
+    for k in range(max(0, args.warmup - 1)):
+        stw = frame(k % fif, wait=True)
+        check(stw, k % fif)
+        warm_kms = stw.kernel_ms
     if args.kernel == "wide" and not instanced:   # built at the first wide render (host binned SAH)
         scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]
     if dist_on:
@@ -330,19 +369,33 @@ def main() -> None:
     rays = kbytes = 0
     kms = 0.0
     spec_visits = 0
-    for _ in range(args.steps):
-        st = frame()
-        check(st)
+    inflight = []
+
+    last_st = ref_st
+
+    def account(st):
+        nonlocal rays, kbytes, kms, spec_visits, last_st
+        last_st = st
         rays += st.rays
         # algorithmic bytes of the tree the kernel traverses: the wide kernel's own visits; the
         # binary kernel's reference-order visits (its speculative extra visits are not work)
         kbytes += st.algo_bytes if args.kernel == "wide" else ref_st.algo_bytes
         spec_visits += st.node_visits
         kms += st.kernel_ms
+
+    for k in range(args.steps):
+        if len(inflight) == fif:   # film k % fif is free once frame k - fif is done (and checked)
+            account(finish(inflight.pop(0)))
+        frame(k % fif)
+        inflight.append(k % fif)
+    for j in inflight:
+        account(finish(j))
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    last = (args.steps - 1) % fif if args.steps > 0 else 0
+    st = last_st   # (the last timed frame's counters)
 
     t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if dist_on:
@@ -374,16 +427,18 @@ def main() -> None:
 
     if rank == 0:
         if dist_on:   # un-permute the stripes of the last frame (rank 0 holds the full image)
-            img = ptdist.assemble(gathered, h, w, STRIPE, world, chans)
+            img = ptdist.assemble(gathered[last], h, w, STRIPE, world, chans)
             torch.cuda.synchronize(dev)
         else:
-            img = local_buf[: h * w * chans]
+            img = local_bufs[last][: h * w * chans]
         if args.png:
             a = img.reshape(-1).cpu().numpy()
             if rgba8:
                 ptamd.write_png_rgba8(args.png, a, w, h)
             else:
                 ptamd.write_png(args.png, a, w, h)
+        if fif > 1 and args.steps > 0:   # overlapped launches: the launch time of one that ran alone
+            kms = warm_kms * args.steps
         achieved = (kbytes / 1e9) / (kms / 1e3) if kms > 0 else 0.0
         rng_desc = (("sample mode: XORWOW per pixel-sample seeded by Philox4x32-10, summation "
                      f"block {args.chunk or max(16, -(-spp // 64))}") if sample else
@@ -409,7 +464,7 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic: scene assembled from the reference's bundled OBJ models (models/), fixed seed",
             "config": {"workload": workload, "width": w, "height": h, "spp": spp, "max_depth": depth,
-                       "stripe_rows": STRIPE, "parallelism": f"rows{world}",
+                       "stripe_rows": STRIPE, "parallelism": f"rows{world}", "frames_in_flight": fif,
                        "output": ("rgba8: quantised on the device like PngImage::saveColor, gathered at 4 B/pixel"
                                   if rgba8 else "f32 RGB, gathered at 12 B/pixel"),
                        "rays_per_frame": total_rays / args.steps,
