@@ -2321,6 +2321,285 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
     waveReduceAdd(counters + 3, c.spheres);
 }
 
+// Queued closest-hit kernels (the default for pt_trace_closest; PT_TRACE_STRIDE=1 selects the
+// grid-stride kernels above).  Persistent waves with a wave-level ray queue (Aila & Laine 2009,
+// "persistent while-while" with dynamic fetch): a lane whose ray has finished takes the next
+// ray of the batch at the top of the next loop iteration instead of idling until the wave's
+// slowest ray is done.  The lanes that ask are ranked by a ballot and an mbcnt prefix count and
+// served, in lane order, from the wave's pool of kTraceGrab consecutive rays (one returning
+// atomic per pool on a queue word of the scene's counters).  Each loop iteration runs one
+// traversal step per lane -- the reference order's node visit with its leaf tests (traceKernel),
+// or the wide tree's primitive group + next node (traceKernelWide) -- with exactly those
+// kernels' arithmetic, so every hit record and work counter is the same.
+#ifndef PT_TRACE_GRAB
+#define PT_TRACE_GRAB 256   // rays per queue grab (a wave's pool)
+#endif
+constexpr uint32_t kTraceGrab = PT_TRACE_GRAB;
+constexpr int kTraceQueue = 24;   // counters[24]: the ray queue (zeroed with the counters before each trace)
+
+// Hand rays to the lanes that have none (`ray` < 0): ballot of the askers, each asker's rank among
+// them (mbcnt), one pool refill by the first asker when the pool is empty.  poolBase / poolLeft /
+// more are wave-uniform; `took` is set for a lane that received ray `ray` (< n).
+#define PT_TRACE_REFILL(took)                                                                       \
+    do {                                                                                          \
+        for (;;) {                                                                                \
+            const uint64_t m_ = __ballot(ray < 0 && more);                                        \
+            if (m_ == 0) break;                                                                   \
+            if (poolLeft == 0u) {                                                                 \
+                const int leader_ = __ffsll((unsigned long long)m_) - 1;                          \
+                unsigned long long b_ = 0;                                                        \
+                if (lane == leader_) b_ = atomicAdd(counters + kTraceQueue, (unsigned long long)kTraceGrab); \
+                const uint32_t lo_ = (uint32_t)__shfl((int)(uint32_t)b_, leader_);                \
+                const uint32_t hi_ = (uint32_t)__shfl((int)(uint32_t)(b_ >> 32), leader_);         \
+                poolBase = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane(hi_) << 32) |       \
+                                     __builtin_amdgcn_readfirstlane(lo_));                        \
+                poolLeft = kTraceGrab;                                                            \
+                if (poolBase >= n) { more = false; break; }                                       \
+            }                                                                                     \
+            const uint32_t take_ = min((uint32_t)__popcll(m_), poolLeft);                         \
+            const uint32_t k_ = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m_ >> 32),         \
+                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m_, 0u));                 \
+            if (ray < 0 && k_ < take_ && poolBase + (int64_t)k_ < n) {                            \
+                ray = poolBase + (int64_t)k_;                                                     \
+                took = true;                                                                      \
+            }                                                                                     \
+            poolBase += take_;                                                                    \
+            poolLeft -= take_;                                                                    \
+            if (poolBase >= n) more = false;                                                      \
+        }                                                                                         \
+    } while (0)
+
+// traceKernel (the reference's order, render_manager.h:86-135) with the ray queue: one node visit
+// (both children's slab tests and leaf tests, trace<STACK>) per lane and iteration.
+template <int STACK>
+__global__ __launch_bounds__(kWave) void traceKernelQ(DevScene S, const pt_ray* rays, int64_t n, float tmin,
+                                                      float tmax, pt_hit* hits, unsigned long long* counters) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    uint32_t* my = stk + lane;
+    Counters c{0, 0, 0, 0};
+    int64_t ray = -1, poolBase = 0;
+    uint32_t poolLeft = 0u;
+    bool more = true;
+    float3 o = f3(0.0f, 0.0f, 0.0f), d = o, inv = o;
+    float closest = 0.0f;
+    int best = -1, node = 0, sp = 0, guard = 0;
+    for (;;) {
+        bool took = false;
+        PT_TRACE_REFILL(took);
+        if (__ballot(ray >= 0) == 0) break;
+        if (ray < 0) continue;
+        bool fin = false;
+        if (took) {   // the query's start (trace<STACK>)
+            const pt_ray r = rays[ray];
+            o = f3(r.o[0], r.o[1], r.o[2]);
+            d = f3(r.d[0], r.d[1], r.d[2]);
+            closest = tmax;
+            best = -1;
+            c.rays++;
+            if (S.nprims <= 1) {
+                if (S.nprims == 1) {   // root is a leaf: tested without a box test (:92-98)
+                    const uint32_t ref = kLeafBit | (__float_as_uint(S.prims[2].w) ? kSphereBit : 0u);
+                    primTest(S, ref, o, d, tmin, closest, best, c);
+                }
+                fin = true;
+            } else {
+                inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                node = 0;
+                sp = 0;
+                guard = 0;
+            }
+        }
+        if (!fin) {   // one node visit of trace<STACK>
+            if (++guard > S.nprims) { atomicOr(S.err, 1u); fin = true; }
+            else {
+                c.visits++;
+                const float4* np = S.nodes + 4 * (size_t)node;
+                const float4 a = np[0], b = np[1], q = np[2], rr = np[3];
+                const uint32_t lref = __float_as_uint(rr.x), rref = __float_as_uint(rr.y);
+                if (slabLeft(a, b, o, inv, tmin, closest).hit) {
+                    if (lref & kLeafBit) primTest(S, lref, o, d, tmin, closest, best, c);
+                    else if (sp < STACK) { my[sp * kWave] = lref; sp++; }
+                    else { atomicOr(S.err, 2u); fin = true; }
+                }
+                if (!fin && slabRight(b, q, o, inv, tmin, closest).hit) {
+                    if (rref & kLeafBit) primTest(S, rref, o, d, tmin, closest, best, c);
+                    else if (sp < STACK) { my[sp * kWave] = rref; sp++; }
+                    else { atomicOr(S.err, 2u); fin = true; }
+                }
+                if (!fin) {
+                    if (sp == 0) fin = true;
+                    else { sp--; node = (int)my[sp * kWave]; }
+                }
+            }
+        }
+        if (fin) {   // the hit record (traceKernel)
+            pt_hit h = {};
+            h.obj = -1;
+            h.mat = -1;
+            if (best >= 0) {
+                HitRec hr = makeHit(S, best, closest, o, d);
+                h.hit = 1;
+                h.obj = hr.obj;
+                h.mat = hr.mat;
+                h.front_face = hr.front ? 1 : 0;
+                h.t = closest;
+                h.p[0] = hr.p.x; h.p[1] = hr.p.y; h.p[2] = hr.p.z;
+                h.n[0] = hr.n.x; h.n[1] = hr.n.y; h.n[2] = hr.n.z;
+            }
+            hits[ray] = h;
+            ray = -1;
+        }
+    }
+    waveReduceAdd(counters + 0, c.rays);
+    waveReduceAdd(counters + 1, c.visits);
+    waveReduceAdd(counters + 2, c.tris);
+    waveReduceAdd(counters + 3, c.spheres);
+}
+
+// traceKernelWide with the ray queue: per lane and iteration, the current primitive group's tests
+// and one node (or instance entry) of the wide traversal.
+template <int STACK, bool INST>
+__global__ __launch_bounds__(kWave) void traceKernelWideQ(DevScene S, const pt_ray* rays, int64_t n, float tmin,
+                                                          float tmax, pt_hit* hits, unsigned long long* counters) {
+    __shared__ uint32_t stk[STACK * kWave];
+    const int lane = threadIdx.x;
+    uint32_t* my = stk + lane;
+    const __amdgpu_buffer_rsrc_t nodeRsrc = rawRsrc(S.wnodes);
+    Counters c{0, 0, 0, 0};
+    int64_t ray = -1, poolBase = 0;
+    uint32_t poolLeft = 0u;
+    bool more = true;
+    float3 wo2 = f3(0.0f, 0.0f, 0.0f), wd = wo2, winv = wo2, o = wo2, d = wo2, inv = wo2;
+    uint32_t woct = 0u, oct = 0u, inst = 0u, ng = 0u, tgBase = 0u, tg = 0u;
+    float shift = 0.0f, tminI = 0.0f, closest = 0.0f, bestLo = 0.0f;
+    int best = -1, sp = 0;
+    bool redo = false;
+    for (;;) {
+        bool took = false;
+        PT_TRACE_REFILL(took);
+        if (__ballot(ray >= 0) == 0) break;
+        if (ray < 0) continue;
+        if (took) {   // the query's start (traceKernelWide)
+            const pt_ray r = rays[ray];
+            const float3 wo = f3(r.o[0], r.o[1], r.o[2]);
+            wd = f3(r.d[0], r.d[1], r.d[2]);
+            winv = f3(rcpRN(wd.x), rcpRN(wd.y), rcpRN(wd.z));
+            woct = (winv.x < 0.0f ? 1u : 0u) | (winv.y < 0.0f ? 2u : 0u) | (winv.z < 0.0f ? 4u : 0u);
+            o = wo; d = wd; inv = winv;
+            oct = woct;
+            inst = 0u;
+            const bool far = !INST && (wideFar(S, o) || (PT_WIDE_MIX && mixUnsafe(winv, S.mixLim)));
+            wo2 = wo;
+            shift = (INST && instFar(S, wo)) ? instEntry(S.cx, S.cy, S.cz, S.ext, wo2, wd, winv) : 0.0f;
+            if (INST) o = wo2;
+            tminI = tmin - shift;
+            closest = tmax - shift;
+            best = -1;
+            sp = 0;
+            redo = far;
+            bestLo = -__builtin_inff();
+            ng = S.nprims > 0 && !far ? (1u << oct) : 0u;
+            tgBase = 0u;
+            tg = 0u;
+            c.rays++;
+        }
+        while (tg) {
+            const uint32_t k = tgBase + (uint32_t)__builtin_ctz(tg);
+            tg &= tg - 1u;
+            const float4* w = S.wprims + 3 * (size_t)k;
+            const Prim q{w[0], w[1], w[2]};
+            if (__float_as_uint(q.p2.w) != 0u) c.spheres++;
+            else c.tris++;
+            const bool lb = !INST && S.nprims > 1;
+            const uint32_t kh = INST ? inst << S.gBits : 0u;
+            if (S.hasSpheres) wideTest<true>(q, o, d, inv, tminI, closest, best, bestLo, lb, redo, kh);
+            else wideTest<false>(q, o, d, inv, tminI, closest, best, bestLo, lb, redo, kh);
+        }
+        bool fin = false;
+        if constexpr (INST) {   // pop; a marker returns to the world ray
+            while ((ng & 0xffu) == 0u && sp > 0) {
+                sp--;
+                ng = my[sp * kWave];
+                if (ng == kInstMarker) { o = wo2; d = wd; inv = winv; oct = woct; ng = 0u; }
+            }
+            if ((ng & 0xffu) == 0u) fin = true;
+        } else if ((ng & 0xffu) == 0u) {
+            if (sp == 0) fin = true;
+            else { sp--; ng = my[sp * kWave]; }
+        }
+        if (!fin) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(ng & 0xffu);
+            const uint32_t child = (ng >> 8) + (bit ^ oct);
+            ng &= ~(1u << bit);
+            if (ng & 0xffu) {
+                if (sp >= STACK) { atomicOr(S.err, 2u); fin = true; }
+                else { my[sp * kWave] = ng; sp++; }
+            }
+            if (!fin) {
+                c.visits++;
+                const uint32_t off = mul80(child);
+                const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
+                const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
+                const uint4 n2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 32u, 0, 0));
+                const uint4 n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
+                const uint4 n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
+                if (INST && n0.w == kInstFlag) {   // an instance: into its object space and bottom-level tree
+                    if (n0.x == 0u) {
+                        const float4 r0 = __builtin_bit_cast(float4, n2), r1 = __builtin_bit_cast(float4, n3),
+                                     r2 = __builtin_bit_cast(float4, n4);
+                        o = xformPoint(r0, r1, r2, wo2);
+                        d = xformDir(r0, r1, r2, wd);
+                        inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));
+                        oct = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u);
+                    }
+                    if (sp >= STACK) { atomicOr(S.err, 2u); fin = true; }
+                    else {
+                        my[sp * kWave] = kInstMarker;
+                        sp++;
+                        ng = (n1.x << 8) | (1u << oct);
+                        inst = n1.y;
+                        tg = 0u;
+                    }
+                } else {
+                    const uint32_t h = wideHits<!INST && PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest);
+                    ng = (n1.x << 8) | (h >> 24);
+                    tgBase = n1.y;
+                    tg = h & 0xffffffu;
+                }
+            }
+        }
+        if (fin) {   // the reference-order redo and the hit record (traceKernelWide)
+            if (redo) {
+                closest = tmax;
+                const int k = traceRefStackless(S, o, d, tmin, closest);
+                best = k >= 0 ? (int)S.rankOf[k] : -1;
+            }
+            pt_hit hr = {};
+            hr.obj = -1;
+            hr.mat = -1;
+            if (best >= 0) {
+                int obj = 0;
+                HitRec x = INST ? makeHitInst(S, (uint32_t)best & kPrimMask, closest, wo2, wd, obj)
+                                : makeHitFrom(S.wshade, best & (int)kPrimMask, closest, o, d);
+                hr.hit = 1;
+                hr.obj = x.obj;
+                hr.mat = x.mat;
+                hr.front_face = x.front ? 1 : 0;
+                hr.t = INST ? closest + shift : closest;
+                hr.p[0] = x.p.x; hr.p[1] = x.p.y; hr.p[2] = x.p.z;
+                hr.n[0] = x.n.x; hr.n[1] = x.n.y; hr.n[2] = x.n.z;
+            }
+            hits[ray] = hr;
+            ray = -1;
+        }
+    }
+    waveReduceAdd(counters + 0, c.rays);
+    waveReduceAdd(counters + 1, c.visits);
+    waveReduceAdd(counters + 2, c.tris);
+    waveReduceAdd(counters + 3, c.spheres);
+}
+
 // initRandom (main.cu:262-269): curand_init(seed, pixel, 0).  The subsequence skip is the
 // GF(2) product of jump matrices J_k = M^(2^(67+k)) for the set bits of the pixel index.
 // Loops are wave-uniform (k, j); column loads are uniform, hence scalar.
@@ -3315,6 +3594,34 @@ int dispatchTrace(int stack, bool wide, const DevScene& S, const pt_ray* r, int6
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const unsigned blocks = (unsigned)std::min<int64_t>((n + kWave - 1) / kWave, (int64_t)cus * 32);
+    const char* strideEnv = std::getenv("PT_TRACE_STRIDE");   // 1: the grid-stride kernels (A/B)
+    if (!(strideEnv && std::atoi(strideEnv) != 0)) {   // default: the queued kernels
+        if (wide) {
+            switch (stack) {
+                case 8: S.winst ? traceKernelWideQ<8, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt)
+                                : traceKernelWideQ<8, false><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                case 16: S.winst ? traceKernelWideQ<16, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt)
+                                 : traceKernelWideQ<16, false><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                case 24: S.winst ? traceKernelWideQ<24, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt)
+                                 : traceKernelWideQ<24, false><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                default: return fail(PT_ERR_STATE, "unsupported wide BVH depth");
+            }
+        } else {
+            switch (stack) {
+                case 16: traceKernelQ<16><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+#if PT_STACK24
+                case 24: traceKernelQ<24><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+#endif
+                case 32: traceKernelQ<32><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                case 48: traceKernelQ<48><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                case 64: traceKernelQ<64><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                case 80: traceKernelQ<80><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
+                default: return fail(PT_ERR_STATE, "unsupported BVH depth");
+            }
+        }
+        HIP_TRY(hipGetLastError());
+        return PT_OK;
+    }
     if (wide && S.winst) {
         switch (stack) {
             case 8: traceKernelWide<8, true><<<blocks, kWave, 0, st>>>(S, r, n, tmin, tmax, h, cnt); break;
