@@ -2335,6 +2335,9 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
 #define PT_TRACE_GRAB 256   // rays per queue grab (a wave's pool)
 #endif
 constexpr uint32_t kTraceGrab = PT_TRACE_GRAB;
+#ifndef PT_TRACE_WAVES
+#define PT_TRACE_WAVES 1   // occupancy target of the queued trace kernels (waves per SIMD; 1 = the compiler's choice)
+#endif
 constexpr int kTraceQueue = 24;   // counters[24]: the ray queue (zeroed with the counters before each trace)
 
 // Hand rays to the lanes that have none (`ray` < 0): ballot of the askers, each asker's rank among
@@ -2372,7 +2375,7 @@ constexpr int kTraceQueue = 24;   // counters[24]: the ray queue (zeroed with th
 // traceKernel (the reference's order, render_manager.h:86-135) with the ray queue: one node visit
 // (both children's slab tests and leaf tests, trace<STACK>) per lane and iteration.
 template <int STACK>
-__global__ __launch_bounds__(kWave) void traceKernelQ(DevScene S, const pt_ray* rays, int64_t n, float tmin,
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES))) void traceKernelQ(DevScene S, const pt_ray* rays, int64_t n, float tmin,
                                                       float tmax, pt_hit* hits, unsigned long long* counters) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;
@@ -2460,7 +2463,7 @@ __global__ __launch_bounds__(kWave) void traceKernelQ(DevScene S, const pt_ray* 
 // traceKernelWide with the ray queue: per lane and iteration, the current primitive group's tests
 // and one node (or instance entry) of the wide traversal.
 template <int STACK, bool INST>
-__global__ __launch_bounds__(kWave) void traceKernelWideQ(DevScene S, const pt_ray* rays, int64_t n, float tmin,
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_WAVES))) void traceKernelWideQ(DevScene S, const pt_ray* rays, int64_t n, float tmin,
                                                           float tmax, pt_hit* hits, unsigned long long* counters) {
     __shared__ uint32_t stk[STACK * kWave];
     const int lane = threadIdx.x;

@@ -15,6 +15,15 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+
+def free_port() -> str:
+    """A free TCP port on 127.0.0.1 for a torch.distributed.run rendezvous (a fixed port can still be
+    held by an earlier run on a shared box)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return str(sk.getsockname()[1])
+
 W, H, DEPTH = 40, 24, 50
 
 
@@ -194,7 +203,7 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     assert r1.returncode == 0, r1.stderr[-2000:]
     env = dict(os.environ, PT_DIST_BACKEND="gloo")
     r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                         "--master-addr", "127.0.0.1", "--master-port", "29517"] + common[:1] + ["--gpus", "2"] +
+                         "--master-addr", "127.0.0.1", "--master-port", free_port()] + common[:1] + ["--gpus", "2"] +
                         common[1:] + ["--png", two], cwd=repo, capture_output=True, text=True, timeout=300, env=env)
     assert r2.returncode == 0, r2.stderr[-2000:]
     np.testing.assert_array_equal(read_png(one), read_png(two))
@@ -218,7 +227,7 @@ def test_bench_rccl_gather_one_rank(tmp_path):
     assert r1.returncode == 0, r1.stderr[-2000:]
     env = dict(os.environ, PT_DIST_FORCE="1", PT_DIST_BACKEND="nccl")
     r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-                         "--master-addr", "127.0.0.1", "--master-port", "29519"] + common[:1] + ["--gpus", "1"] +
+                         "--master-addr", "127.0.0.1", "--master-port", free_port()] + common[:1] + ["--gpus", "1"] +
                         common[1:] + ["--png", forced], cwd=repo, capture_output=True, text=True, timeout=300, env=env)
     assert r2.returncode == 0, r2.stderr[-2000:]
     np.testing.assert_array_equal(read_png(one), read_png(forced))
@@ -247,7 +256,7 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     assert r1.returncode == 0, r1.stderr[-2000:]
     env = dict(os.environ, PT_DIST_BACKEND="gloo")
     r8 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
-                         "--master-addr", "127.0.0.1", "--master-port", "29518"] + common[:1] + ["--gpus", "8"] +
+                         "--master-addr", "127.0.0.1", "--master-port", free_port()] + common[:1] + ["--gpus", "8"] +
                         common[1:] + ["--png", eight], cwd=repo, capture_output=True, text=True, timeout=600, env=env)
     assert r8.returncode == 0, r8.stderr[-2000:]
     np.testing.assert_array_equal(read_png(one), read_png(eight))
