@@ -24,6 +24,7 @@ def free_port() -> str:
         sk.bind(("127.0.0.1", 0))
         return str(sk.getsockname()[1])
 
+
 W, H, DEPTH = 40, 24, 50
 
 
