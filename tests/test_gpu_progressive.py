@@ -210,10 +210,13 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     np.testing.assert_array_equal(read_png(one), read_png(two))
 
 
-def test_bench_rccl_gather_one_rank(tmp_path):
+@pytest.mark.parametrize("fif", [1, 2])
+def test_bench_rccl_gather_one_rank(tmp_path, fif):
     """bench.py's multi-rank flow over RCCL (backend "nccl": process group, dist.gather of the
     RGBA8 stripes, barriers, max / sum reductions) with the one rank a one-GPU box allows
-    (PT_DIST_FORCE=1): the PNG equals the plain 1-rank PNG and the reported rays are the frame's."""
+    (PT_DIST_FORCE=1): the PNG equals the plain 1-rank PNG and the reported rays are the frame's.
+    fif 2: frames in flight as N > 1 runs them (two films on two streams, each frame's gather
+    enqueued on its own stream, three timed frames so both films alternate)."""
     import json
     import os
     import subprocess
@@ -229,12 +232,14 @@ def test_bench_rccl_gather_one_rank(tmp_path):
     env = dict(os.environ, PT_DIST_FORCE="1", PT_DIST_BACKEND="nccl")
     r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
                          "--master-addr", "127.0.0.1", "--master-port", free_port()] + common[:1] + ["--gpus", "1"] +
-                        common[1:] + ["--png", forced], cwd=repo, capture_output=True, text=True, timeout=300, env=env)
+                        common[1:] + ["--png", forced, "--frames-in-flight", str(fif), "--steps", "3"], cwd=repo,
+                        capture_output=True, text=True, timeout=300, env=env)
     assert r2.returncode == 0, r2.stderr[-2000:]
     np.testing.assert_array_equal(read_png(one), read_png(forced))
     a = json.loads(r1.stdout.strip().splitlines()[-1])
     b = json.loads(r2.stdout.strip().splitlines()[-1])
     assert a["config"]["rays_per_frame"] == b["config"]["rays_per_frame"] > 0
+    assert b["config"]["frames_in_flight"] == fif and b["steps"] == 3
 
 
 def test_bench_c4_eight_ranks_rehearsal(tmp_path):
