@@ -2335,6 +2335,9 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
 #define PT_TRACE_GRAB 256   // rays per queue grab (a wave's pool)
 #endif
 constexpr uint32_t kTraceGrab = PT_TRACE_GRAB;
+#ifndef PT_TRACE_DIAG_REDO
+#define PT_TRACE_DIAG_REDO 0   // diagnostic builds: count the queries that take the reference-order redo as sphere tests
+#endif
 #ifndef PT_TRACE_WAVES
 #define PT_TRACE_WAVES 1   // occupancy target of the queued trace kernels (waves per SIMD; 1 = the compiler's choice)
 #endif
@@ -2573,6 +2576,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_
             }
         }
         if (fin) {   // the reference-order redo and the hit record (traceKernelWide)
+            if (PT_TRACE_DIAG_REDO && redo) c.spheres++;
             if (redo) {
                 closest = tmax;
                 const int k = traceRefStackless(S, o, d, tmin, closest);
