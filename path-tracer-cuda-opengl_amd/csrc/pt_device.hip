@@ -2338,6 +2338,9 @@ constexpr uint32_t kTraceGrab = PT_TRACE_GRAB;
 #ifndef PT_TRACE_DIAG_REDO
 #define PT_TRACE_DIAG_REDO 0   // diagnostic builds: count the queries that take the reference-order redo as sphere tests
 #endif
+#ifndef PT_TRACE_DIAG_VISITS
+#define PT_TRACE_DIAG_VISITS 0   // diagnostic builds: each hit record's `mat` = the query's wide node visits
+#endif
 #ifndef PT_TRACE_WAVES
 #define PT_TRACE_WAVES 1   // occupancy target of the queued trace kernels (waves per SIMD; 1 = the compiler's choice)
 #endif
@@ -2481,6 +2484,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_
     float shift = 0.0f, tminI = 0.0f, closest = 0.0f, bestLo = 0.0f;
     int best = -1, sp = 0;
     bool redo = false;
+    uint32_t qVisits = 0u;   // (PT_TRACE_DIAG_VISITS)
     for (;;) {
         bool took = false;
         PT_TRACE_REFILL(took);
@@ -2509,6 +2513,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_
             tgBase = 0u;
             tg = 0u;
             c.rays++;
+            qVisits = 0u;
         }
         while (tg) {
             const uint32_t k = tgBase + (uint32_t)__builtin_ctz(tg);
@@ -2544,6 +2549,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_
             }
             if (!fin) {
                 c.visits++;
+                qVisits++;
                 const uint32_t off = mul80(child);
                 const uint4 n0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off, 0, 0));
                 const uint4 n1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 16u, 0, 0));
@@ -2597,6 +2603,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_
                 hr.p[0] = x.p.x; hr.p[1] = x.p.y; hr.p[2] = x.p.z;
                 hr.n[0] = x.n.x; hr.n[1] = x.n.y; hr.n[2] = x.n.z;
             }
+            if (PT_TRACE_DIAG_VISITS) hr.mat = (int)qVisits;
             hits[ray] = hr;
             ray = -1;
         }
