@@ -104,44 +104,58 @@ def cpu_facts() -> dict:
             "cpu_model": model, "usable_cpus": usable}
 
 
-def cpu_baseline(preset, budget_s: float = 12.0, gpu_ref=None) -> dict:
+def cpu_baseline(preset, budget_s: float = 12.0, gpu_ref=None, spp: int = 0, legs=None) -> dict:
     """Oracle (scalar C++ port of the reference path, std::thread over rows) on a bounded sample:
     the full frame at 1 spp per pass, passes repeated until `budget_s` of CPU work.  One thread per
     CPU this process may use (the affinity mask / cgroup quota: on the GPU pool the box's share of
     its machine, whose nproc is larger -- both are recorded); the host's timing in the reference is
-    std::clock around render (main.cu:469-476).  Beside the rate: the CPU traversal's node visits
-    and primitive tests per ray (binary LBVH, the reference's order) and the GPU's counts for the
-    same scene (reference-order kernel and the wide kernel), as BASELINE.md section 4 asks."""
+    std::clock around render (main.cu:469-476).  BASELINE.md section 4 asks for ms/frame at the
+    config's sample count: `ms_per_frame_extrapolated` = the measured time of one 1-spp pass x spp
+    (a pass is the whole frame at 1 spp; samples are independent, so time is linear in spp).
+    Beside the rate: the CPU traversal's node visits and primitive tests per ray (binary LBVH, the
+    reference's order) and the GPU's counts for the same scene (reference-order kernel and the wide
+    kernel).  `legs`: {config: (preset, spp, budget_s)} -- the same measurement, shorter, on other
+    BASELINE configurations."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
 
     facts = cpu_facts()
     threads = int(os.environ.get("PT_CPU_THREADS", "0")) or facts["usable_cpus"]
-    w, h = preset.width, preset.height
-    nodes = oracle.build_lbvh(preset.objects, oracle.morton_keys(preset.objects), tight=True)
-    rows = np.arange(h, dtype=np.int32)
-    states = oracle.film_states(1, w, rows)
-    cam = ptamd.camera_to_array(preset.camera)
-    rays = visits = tris = sphs = 0
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        _, st = oracle.render(preset.objects, preset.materials, nodes, cam, w, h, rows, 1, preset.max_depth,
-                              states, nthreads=threads)
-        rays += st.rays
-        visits += st.node_visits
-        tris += st.tri_tests
-        sphs += st.sphere_tests
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    out = {"value": rays / el / 1e6, "unit": "Mray/s", "cores": threads, "threads": threads, "kind": "port",
-           "sample": f"{preset.name} {w}x{h}, {passes} pass(es) of 1 spp depth {preset.max_depth} "
-                     f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads",
-           "per_ray": {"cpu_node_visits": visits / max(rays, 1), "cpu_prim_tests": (tris + sphs) / max(rays, 1)}}
+
+    def leg(p, budget, spp_full):
+        w, h = p.width, p.height
+        nodes = oracle.build_lbvh(p.objects, oracle.morton_keys(p.objects), tight=True)
+        rows = np.arange(h, dtype=np.int32)
+        states = oracle.film_states(1, w, rows)
+        cam = ptamd.camera_to_array(p.camera)
+        rays = visits = tris = sphs = 0
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            _, st = oracle.render(p.objects, p.materials, nodes, cam, w, h, rows, 1, p.max_depth, states,
+                                  nthreads=threads)
+            rays += st.rays
+            visits += st.node_visits
+            tris += st.tri_tests
+            sphs += st.sphere_tests
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                break
+        return {"value": rays / el / 1e6, "unit": "Mray/s",
+                "ms_per_frame_extrapolated": el / passes * spp_full * 1e3, "spp": spp_full,
+                "sample": f"{p.name} {w}x{h}, {passes} pass(es) of 1 spp depth {p.max_depth} "
+                          f"({rays} rays, {el:.1f} s), oracle/ scalar C++ on {threads} threads",
+                "per_ray": {"cpu_node_visits": visits / max(rays, 1), "cpu_prim_tests": (tris + sphs) / max(rays, 1)}}
+
+    out = leg(preset, budget_s, spp or preset.spp)
+    out.update({"cores": threads, "threads": threads, "kind": "port",
+                "ms_per_frame_note": "time of one 1-spp pass over the whole frame x the config's spp (the "
+                                     "reference's own timing is std::clock around render, main.cu:469-476)"})
     out.update(facts)
     if gpu_ref:
         out["per_ray"].update(gpu_ref)
+    if legs:
+        out["legs"] = {k: leg(p, b, s) for k, (p, s, b) in legs.items()}
     return out
 
 
@@ -259,16 +273,43 @@ def main() -> None:
     # one rank -- a one-GPU box can run the RCCL gather of a real frame (never a reported number)
     dist_on = world > 1 or os.environ.get("PT_DIST_FORCE") == "1"
     if dist_on:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        # every collective times out (PT_DIST_TIMEOUT, default 120 s) and a rank that spends longer
+        # than PT_BENCH_WATCHDOG s (default 600 for N > 1) in one phase dumps its stacks and exits
+        ptdist.init(backend, rank, world, device=dev if backend == "nccl" else None,
+                    timeout_s=float(os.environ.get("PT_DIST_TIMEOUT", "120")),
+                    watchdog_s=float(os.environ.get("PT_BENCH_WATCHDOG", "600" if world > 1 else "0")))
+        with ptdist.guarded():   # any failure on a rank ends it at once, naming rank and phase
+            run(args, world, rank, local, backend, dev, dist_on)
+    else:
+        run(args, world, rank, local, backend, dev, dist_on)
+
+
+def injected(rank: int, where: str) -> str:
+    """Test hook (tests/test_gpu_progressive.py): PT_BENCH_INJECT=<rank>:<where>:<kind> makes that
+    rank fail at that point -- kind `raise` (an exception), `mismatch` (a frame check that fails) or
+    `hang` (stops responding) -- to show that every rank then exits non-zero within the timeout."""
+    spec = os.environ.get("PT_BENCH_INJECT", "")
+    if not spec:
+        return ""
+    r, w, kind = spec.split(":")
+    if int(r) != rank or w != where:
+        return ""
+    if kind == "raise":
+        raise RuntimeError(f"injected failure on rank {rank} at {where}")
+    if kind == "hang":
+        time.sleep(10 ** 6)
+    return kind
+
+
+def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: bool) -> None:
+    phase = ptdist.phase
 
     if world > 1 and "PT_BUILD_THREADS" not in os.environ:
         # the ranks of a node share its host cores: each rank's host wide-tree build (before the
         # timed frames) takes its share of them instead of 16 threads each
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
         os.environ["PT_BUILD_THREADS"] = str(max(1, cpu_facts()["usable_cpus"] // max(1, local_world)))
+    phase("scene build")
     name, workload = CONFIGS[args.config]
     instanced = args.config in INSTANCED
     if instanced and args.kernel != "wide":
@@ -282,9 +323,15 @@ def main() -> None:
         scene.build_bvh()
         scene_build = {"two_level_tree_host_ms": scene.build_ms, "device_bytes": scene.bvh_info()["device_bytes"]}
     else:
-        scene = ptamd.Scene(preset.objects, preset.materials, device=local)
-        scene.build_bvh()   # again: the first build in a process also pays one-time module loading
-        scene_build = {"lbvh_device_ms": scene.build_ms}
+        # N > 1: every rank builds the wide tree on its own GPU (PT_BVH_WIDE_DEVICE: top-down SAH, the
+        # host build's quality, C5 7 ms) instead of 8 ranks sharing the node's host cores for the host
+        # SAH build (C5 0.75 s on 16 threads); the frames are the same (closest hits do not depend on
+        # the tree).  PT_BENCH_WIDE_DEVICE=0/1 overrides.
+        wide_dev = os.environ.get("PT_BENCH_WIDE_DEVICE", "1" if world > 1 else "0") == "1"
+        flags = ptamd.PT_BVH_ORIGIN_BOUNDS | (ptamd.PT_BVH_WIDE_DEVICE if wide_dev else 0)
+        scene = ptamd.Scene(preset.objects, preset.materials, device=local, flags=flags)
+        scene.build_bvh(flags)   # again: the first build in a process also pays one-time module loading
+        scene_build = {"lbvh_device_ms" if not wide_dev else "lbvh_plus_wide_tree_device_ms": scene.build_ms}
     # Frames in flight (N > 1; --frames-in-flight): consecutive steps alternate between two films
     # (and output buffers) on two streams, so a frame's first waves start while the previous
     # frame's last paths finish -- the launch's tail, 7 % of a 1/8 share of C3 but 0.2 % of the
@@ -305,8 +352,10 @@ def main() -> None:
     sample = args.rng == "sample"
 
     kernel_id = ptamd.KERNEL_WIDE if args.kernel == "wide" else ptamd.KERNEL_WAVEFRONT
+    gather_ev = []   # (start, end) HIP events around each timed frame's gather (nccl), read after the loop
+    gather_host_ms = [0.0]   # gloo rehearsal: host time of the gathers
 
-    def frame(j, kernel=kernel_id, wait=False):
+    def frame(j, kernel=kernel_id, wait=False, timed=False):
         # every step renders the SAME frame: streams back to curand_init(seed, pixel, 0)
         # (sample mode is stateless: a pure function of seed, pixel and sample).  Film j, its
         # buffer and stream; wait=False enqueues it (films[j].stats() waits for it).
@@ -320,11 +369,20 @@ def main() -> None:
         if dist_on:   # the frame's stripes to rank 0 (one gather; SURVEY 8(e) ncclGather), after it on its stream
             with torch.cuda.stream(s):
                 if backend == "nccl":
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if timed else None
+                    if ev:
+                        ev[0].record(s)
                     ptdist.gather_to_root(buf, world, rank, gathered[j])
+                    if ev:
+                        ev[1].record(s)
+                        gather_ev.append(ev)
                 else:
+                    tg0 = time.perf_counter()
                     g = ptdist.gather_to_root(buf.cpu(), world, rank)
                     if rank == 0:
                         gathered[j].copy_(g)
+                    if timed:
+                        gather_host_ms[0] += (time.perf_counter() - tg0) * 1e3
         return st
 
     # Warmup 1 uses the ray-synchronous kernel, whose traversal follows the reference's node
@@ -332,36 +390,52 @@ def main() -> None:
     # visit a few extra nodes speculatively; those are not counted as useful work).  Both
     # kernels produce the identical frame (same rays, same primitive tests, same pixels).
     # (An instanced scene has only the wide kernel: its first frame is the one later frames equal.)
+    phase("reference-order frame")
     ref_st = frame(0, ptamd.KERNEL_WIDE if instanced else ptamd.KERNEL_SIMPLE, wait=True)
     ref_buf.copy_(local_bufs[0])
+    failed = []   # this rank's frames that differ from the reference-order frame
 
-    def check(st, j):
-        # every frame: this rank's pixels and ray count equal the reference-order frame's
+    def check(st, j, where):
+        # every frame: this rank's pixels and ray count equal the reference-order frame's.  A
+        # mismatch is recorded, not raised: all ranks learn of it together (agree) and exit with it.
         with torch.cuda.stream(streams[j]):
             same = torch.equal(local_bufs[j], ref_buf)
+        if injected(rank, where) == "mismatch":
+            same = False
         if st.rays != ref_st.rays or not same or (
                 args.kernel == "wavefront" and (st.tri_tests != ref_st.tri_tests or
                                                 st.sphere_tests != ref_st.sphere_tests)):
-            raise SystemExit("frame differs from the reference-order frame")
+            failed.append(where)
 
-    def finish(j):
+    def agree(where):
+        # every rank's checks so far; any failure ends EVERY rank with status 3 (N = 1: this rank)
+        bad = ptdist.agree(not failed, dev if backend == "nccl" else "cpu") if dist_on else ([rank] if failed else [])
+        if bad:
+            raise SystemExit(f"frame differs from the reference-order frame on rank(s) {bad} ({where}; "
+                             f"this rank: {failed or 'ok'})")
+
+    def finish(j, where="timed frames"):
         st = films[j].stats()   # (waits for film j's frame)
-        check(st, j)
+        check(st, j, where)
         return st
 
-    check(ref_st, 0)   # (also loads torch's comparison kernels before the timed region)
+    check(ref_st, 0, "reference-order frame")   # (also loads torch's comparison kernels before the timed region)
     fif = args.frames_in_flight or (2 if world > 1 else 1)
     warm_kms = ref_st.kernel_ms
+    phase("warmup frames")
     if fif == 2:
         st1 = frame(1, wait=True)   # (film 1's first launch: its tile costs for the launch order)
-        check(st1, 1)
+        check(st1, 1, "warmup frames")
         warm_kms = st1.kernel_ms
     for k in range(max(0, args.warmup - 1)):
         stw = frame(k % fif, wait=True)
-        check(stw, k % fif)
+        check(stw, k % fif, "warmup frames")
         warm_kms = stw.kernel_ms
-    if args.kernel == "wide" and not instanced:   # built at the first wide render (host binned SAH)
-        scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]
+    if args.kernel == "wide" and not instanced and "lbvh_plus_wide_tree_device_ms" not in scene_build:
+        scene_build["wide_tree_host_ms"] = scene.wide_info()["build_ms"]   # built at the first wide render (host SAH)
+    agree("warmup")
+    phase("timed frames")
+    injected(rank, "timed")
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -386,7 +460,7 @@ def main() -> None:
     for k in range(args.steps):
         if len(inflight) == fif:   # film k % fif is free once frame k - fif is done (and checked)
             account(finish(inflight.pop(0)))
-        frame(k % fif)
+        frame(k % fif, timed=True)
         inflight.append(k % fif)
     for j in inflight:
         account(finish(j))
@@ -396,16 +470,49 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     last = (args.steps - 1) % fif if args.steps > 0 else 0
     st = last_st   # (the last timed frame's counters)
+    phase("reduce")
+    agree("timed frames")
 
-    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    tdev = dev if backend == "nccl" else "cpu"
+    gather_ms = sum(a.elapsed_time(b) for a, b in gather_ev) if gather_ev else gather_host_ms[0]
+    t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=tdev)
+    per_rank = single_frame_ms = None
     if dist_on:
         mx = t[:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t[1:].clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, total_rays = float(mx.item()), float(sm.item())
+        # per rank: render-kernel ms and gather ms per timed frame (HIP events on the frame's
+        # stream; gloo: host time), rays per frame, wall ms per frame
+        mine = torch.tensor([kms / max(args.steps, 1), gather_ms / max(args.steps, 1), rays / max(args.steps, 1),
+                             t[0].item() / max(args.steps, 1) * 1e3],
+                            dtype=torch.float64, device=tdev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [{"rank": r, "kernel_ms": float(v[0]), "gather_ms": float(v[1]), "rays_per_frame": float(v[2]),
+                     "wall_ms_per_frame": float(v[3])} for r, v in enumerate(torch.stack(allr).cpu().tolist())]
     else:
         total_rays = float(rays)
+    if fif > 1 and args.steps > 0:
+        # one frame alone (no frame in flight beside it): its latency, max over ranks, beside the
+        # pipelined ms_per_step
+        phase("single frame")
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        frame(0)
+        finish(0, "single frame")
+        torch.cuda.synchronize(dev)
+        if dist_on:
+            dist.barrier()
+        sf = torch.tensor([(time.perf_counter() - t1) * 1e3], dtype=torch.float64, device=tdev)
+        if dist_on:
+            dist.all_reduce(sf, op=dist.ReduceOp.MAX)
+        single_frame_ms = float(sf.item())
+        agree("single frame")
+    phase("report")
 
     compat = None
     if sample and world == 1 and not args.no_compat:
@@ -506,6 +613,13 @@ def main() -> None:
                                         "wave_instructions_per_launch": valu, "source": valu_src}},
         }
         out["build_id"] = bid
+        if per_rank is not None:
+            out["per_rank"] = per_rank
+        if single_frame_ms is not None:
+            out["single_frame_ms"] = single_frame_ms
+            out["single_frame_note"] = ("one frame rendered alone after the timed frames (no frame in flight beside "
+                                        "it), max over ranks; ms_per_step is the pipelined rate with "
+                                        f"frames_in_flight {fif}")
         if compat:
             out["compat_mode"] = compat
         if world == 1 and not args.no_interactive:
@@ -525,7 +639,16 @@ def main() -> None:
                 "gpu_wide_prim_tests": (st.tri_tests + st.sphere_tests) / max(st.rays, 1),
                 "note": "node visits: binary LBVH nodes (CPU, reference-order GPU kernel) vs compressed 8-wide "
                         "nodes (wide kernel); CPU at 1 spp (bounded sample), GPU over the whole frame"}
-            out["cpu_baseline"] = cpu_baseline(ptamd.Preset(name) if instanced else preset, gpu_ref=gpu_ref)
+            # short legs on the other single-GPU BASELINE configurations (C2, C5; C3 when the bench
+            # ran another one), BASELINE.md section 4 (PT_CPU_LEGS=0: none)
+            legs = {}
+            if os.environ.get("PT_CPU_LEGS", "1") != "0":
+                for cfg in ("c2", "c3", "c5"):
+                    if CONFIGS[cfg][0] != name:
+                        lp = ptamd.Preset(CONFIGS[cfg][0])
+                        legs[cfg] = (lp, CONFIG_SPP.get(cfg, lp.spp), 3.0)
+            out["cpu_baseline"] = cpu_baseline(ptamd.Preset(name) if instanced else preset, gpu_ref=gpu_ref,
+                                               spp=spp, legs=legs)
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

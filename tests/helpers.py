@@ -141,3 +141,40 @@ def max_stack(nodes: np.ndarray, n: int) -> int:
             todo.append((left, d))
     return best
 
+
+
+def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
+    """subprocess.run for the multi-process tests: stdout and stderr go to one log file (every
+    rank's lines, each tagged by bench.py / ptdist with its rank and phase), the child runs in its
+    own session, and on a timeout the whole process group is killed and the AssertionError carries
+    the log's tail -- so a hang names its rank and phase.  Keep `timeout` below the test's pytest
+    timeout so this report, not pytest-timeout's stack of the parent, is what a hang produces.
+    Returns (returncode, stdout+stderr text, wall seconds)."""
+    import os
+    import signal
+    import subprocess
+    import tempfile
+    import time
+    if log_path is None:
+        log_path = tempfile.mktemp(suffix=".log")
+    t0 = time.perf_counter()
+    with open(log_path, "w+") as log:
+        p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait()
+            log.seek(0)
+            raise AssertionError(f"{' '.join(map(str, cmd[:8]))} ... still running after {timeout} s; log tail:\n"
+                                 + log.read()[-4000:])
+        log.seek(0)
+        return rc, log.read(), time.perf_counter() - t0
+
+
+def last_json(text):
+    import json
+    return json.loads([x for x in text.splitlines() if x.startswith("{")][-1])

@@ -95,3 +95,55 @@ def test_stripe_partition_covers_frame():
         allr = np.sort(np.concatenate(parts))
         np.testing.assert_array_equal(allr, np.arange(h))
         assert max(len(p) for p in parts) <= ptdist.max_rows(h, stripe, world)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("mode", ["none", "raise", "mismatch", "hang"])
+def test_one_failing_rank_ends_every_rank(mode, tmp_path):
+    """bench.py's fail-fast path (ptdist.init / phase / guarded / agree) with 3 gloo ranks: when rank 1
+    fails in phase "frame check" -- an exception, a failed frame check, or a hang -- EVERY rank exits
+    non-zero within the collective timeout (plus process start-up), and the failing rank's stderr
+    names its rank and phase.  With no failure all ranks exit 0 and the gather is complete."""
+    import subprocess
+    import time
+    world, timeout_s, watchdog_s = 3, 8.0, 12.0
+    port = str(_free_port())
+    procs, logs = [], []
+    t0 = time.perf_counter()
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, GLOO_SOCKET_IFNAME="lo")
+        log = open(tmp_path / f"rank{r}.log", "w+")
+        logs.append(log)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "failfast_worker.py"), mode, str(timeout_s),
+                                       str(watchdog_s)], env=env, stdout=log, stderr=subprocess.STDOUT,
+                                      start_new_session=True))
+    limit = 150.0   # start-up (import torch) + the timeout / watchdog, far below this test's own timeout
+    try:
+        for p in procs:
+            p.wait(timeout=max(1.0, limit - (time.perf_counter() - t0)))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, 9)
+        tails = []
+        for r, log in enumerate(logs):
+            log.seek(0)
+            tails.append(f"--- rank {r} (exit {procs[r].poll()}):\n" + log.read()[-1500:])
+        pytest.fail("ranks still running after %.0f s:\n%s" % (limit, "\n".join(tails)))
+    elapsed = time.perf_counter() - t0
+    out = []
+    for log in logs:
+        log.seek(0)
+        out.append(log.read())
+        log.close()
+    codes = [p.returncode for p in procs]
+    if mode == "none":
+        assert codes == [0] * world, out
+        return
+    assert all(c != 0 for c in codes), (codes, out)
+    assert "[rank 1/3] FAILED in phase 'frame check'" in out[1] or mode == "hang", out[1]
+    if mode == "hang":   # the hung rank's watchdog dumps its stack (faulthandler) and ends it
+        assert "time.sleep" in out[1] or "Timeout" in out[1], out[1]
+    # every rank ends within the timeout (the hung rank: its watchdog) after start-up
+    assert elapsed < 120.0, elapsed
