@@ -43,6 +43,7 @@ using pt::fail;
 
 namespace pt {
 int launchCompatWide(int stack, const void* params, hipStream_t st);   // pt_compat.hip
+int compatWideWavesPerCU(int stack, int& n);                            // pt_compat.hip
 }
 
 #define HIP_TRY(expr)                                                                        \
@@ -545,6 +546,49 @@ __device__ __forceinline__ uint32_t wideHits(uint4 n0, uint4 n1, uint4 n2, uint4
     return hits;
 }
 
+// A direction parallel to an axis plane (a component +-0: |1/d| = inf; NaN counts too).
+__device__ __forceinline__ bool zeroAxes(float3 inv) {
+    return !(fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z)) < __builtin_inff());
+}
+// One axis the ray is parallel to (d = +-0, 1/d = +-inf), for the 8 children of a wide node: aabb::hit
+// (aabb.h:21-34) gives (plane - o) * (1/d) = -inf / +inf by the side of each plane o lies on (NaN when
+// on it, which the reference's ternaries skip), so the axis bounds nothing when o lies between a
+// child's two planes and rejects the child otherwise.  wideHits' decomposed form q * (s * inv) +
+// (p - o) * inv is NaN for every plane of such an axis (never a wrong rejection, never a rejection
+// at all: the ray would enter every child it overlaps in the other two axes -- round 4: 1,000-1,500
+// node visits for C5 rays at the height of the origin).  Here the test itself, on the quantised
+// planes p + q * s: u = (o - p) / s (1 / s a power of two), a child is kept when qlo <= u <= qhi.
+// (The rounding of o - p is far below the planes' one-quantum outward margin, as in wideHits.)
+// k0 / k1: the children 0-3 / 4-7 byte masks, cleared (bits 5-7) for rejected children.
+__device__ __forceinline__ void zeroAxisKeep(float oc, uint32_t pbits, uint32_t ebyte, uint32_t qlo0, uint32_t qlo1,
+                                             uint32_t qhi0, uint32_t qhi1, uint32_t& k0, uint32_t& k1) {
+    const float u = (oc - __uint_as_float(pbits)) * __uint_as_float((254u - ebyte) << 23);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const float l0 = (float)((qlo0 >> (8 * j)) & 0xffu), h0 = (float)((qhi0 >> (8 * j)) & 0xffu);
+        const float l1 = (float)((qlo1 >> (8 * j)) & 0xffu), h1 = (float)((qhi1 >> (8 * j)) & 0xffu);
+        if (u < l0 || u > h0) k0 &= ~(0xe0u << (8 * j));   // (NaN u: kept)
+        if (u < l1 || u > h1) k1 &= ~(0xe0u << (8 * j));
+    }
+}
+// Instanced scenes' node test (they have no reference-order query to hand such rays to): a wave with
+// a lane whose ray -- in the current space -- is parallel to an axis plane clears the meta bytes of
+// the children that lane's exact slab test rejects on that axis (zeroAxisKeep), then runs the usual
+// test.  A wave-uniform branch: the common case pays the ballot only, and no registers stay live.
+__device__ __forceinline__ uint32_t wideHitsInst(uint4 n0, uint4 n1, uint4 n2, uint4 n3, uint4 n4, float3 o,
+                                                 float3 inv, uint32_t oct, float tmin, float tmax) {
+    if (__ballot(zeroAxes(inv)) != 0) {
+        const float inf = __builtin_inff();
+        uint32_t k0 = 0xffffffffu, k1 = 0xffffffffu;
+        if (!(fabsf(inv.x) < inf)) zeroAxisKeep(o.x, n0.x, n0.w & 0xffu, n2.x, n2.y, n2.z, n2.w, k0, k1);
+        if (!(fabsf(inv.y) < inf)) zeroAxisKeep(o.y, n0.y, (n0.w >> 8) & 0xffu, n3.x, n3.y, n3.z, n3.w, k0, k1);
+        if (!(fabsf(inv.z) < inf)) zeroAxisKeep(o.z, n0.z, (n0.w >> 16) & 0xffu, n4.x, n4.y, n4.z, n4.w, k0, k1);
+        n1.z &= k0;
+        n1.w &= k1;
+    }
+    return wideHits<false>(n0, n1, n2, n3, n4, o, inv, oct, tmin, tmax);
+}
+
 // The ray origin lies farther than 8 scene extents from the scene's centre on some axis, beyond
 // the distance the wide boxes' margin covers (wideHits): the query runs in the reference's order.
 __device__ __forceinline__ bool wideFar(float cx, float cy, float cz, float ext, float3 o) {
@@ -556,15 +600,18 @@ __device__ __forceinline__ bool wideFar(const DevScene& S, float3 o) { return wi
 // within that reach (buildInstanced), 4x finer planes than 8 extents would allow (c5i 503 -> 498
 // ms); farther origins start at their entry into the world (instEntry).
 constexpr float kInstFarExt = 2.0f;
+static_assert(kInstFarExt >= 1.0f, "instEntry's cube (centre +- ext) must lie inside the quantised reach");
 __device__ __forceinline__ bool instFar(const DevScene& S, float3 o) {
     const float m = fmaxf(fmaxf(fabsf(o.x - S.cx), fabsf(o.y - S.cy)), fabsf(o.z - S.cz));
     return !(m <= kInstFarExt * S.ext);   // (NaN: far)
 }
 
 // Instanced scenes have no reference-order query: a ray whose origin lies beyond the region the
-// planes' margin covers (wideFar) is moved along itself to its entry into the world box grown by one
-// extent on every side -- no geometry lies before that point, and the new origin is within 1.5
-// extents of the centre, inside the region every instanced tree was quantised for (buildInstanced).
+// planes' margin covers (instFar) is moved along itself to its entry into the cube centre +- ext
+// (ext = the world box's LARGEST extent, so the cube is the world box grown by at least ext / 2 on
+// every side) -- no geometry lies before that point, and the new origin lies within 1 extent of the
+// centre (max norm), inside the 2-extent reach every instanced tree was quantised for
+// (buildInstanced; kInstFarExt >= 1 keeps the cube inside that reach).
 // Returns the distance moved (0 when the ray misses that box or starts inside it).
 __device__ __forceinline__ float instEntry(float cx, float cy, float cz, float ext, float3& o, float3 d, float3 inv) {
     const float lx = (cx - ext - o.x) * inv.x, hx = (cx + ext - o.x) * inv.x;
@@ -1181,6 +1228,9 @@ constexpr int kTaskBlocks = PT_TASK_BLOCKS;   // sample mode: summation blocks p
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
+#ifndef PT_COMPAT_QUEUE
+#define PT_COMPAT_QUEUE 0   // compat mode: persistent waves take pixels from a queue (else one wave per tile; 1 measured slower)
+#endif
 #ifndef PT_WIDE_SPEC
 #define PT_WIDE_SPEC 1   // wide kernels: speculative traversal, primitive groups a lane may park while it keeps visiting nodes (0-3)
 #endif
@@ -1278,6 +1328,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Only SHADE steps (per sample, not per node or primitive) touch it, so it lives in LDS, not
     // in four VGPRs carried through every step.
     __shared__ uint4 taskState[SAMPLE ? kWave : 1];
+    // compat mode with the pixel queue (CQ): the lane's pixel {its tile, rays traced for it, its
+    // index} (LDS: only a pixel's first and last sample touch it)
+    constexpr bool CQ = !SAMPLE && PT_COMPAT_QUEUE != 0;
+    __shared__ uint4 pixState[CQ ? kWave : 1];
     // sample mode, tasks of several blocks: the task's closed blocks so far, per lane (x, y, z)
     // (wide kernels; the binary ones take one block per task and keep their LDS for the stack)
     constexpr bool GROUPS = PT_TASK_GROUPS && SAMPLE && WIDE && STACK <= 16;   // (STACK 24: the LDS would cap occupancy)
@@ -1286,21 +1340,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         accPart[threadIdx.x] = 0ull; accPart[kWave + threadIdx.x] = 0ull; accPart[2 * kWave + threadIdx.x] = 0ull;
     }
     const int lane = threadIdx.x;
-    // compat mode: one wave = one tile, all spp of its pixels in order (per-pixel XORWOW streams).
+    // compat mode: all spp of a pixel in order (its per-pixel XORWOW stream).  With the pixel queue
+    // (CQ, default) persistent waves take pixels from a global counter (PT_TAKE_PIXELS): a lane
+    // whose pixel has all its samples takes the next pixel, so no lane idles while its tile's
+    // slowest pixel finishes; otherwise one wave = one tile.
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
     // block) from a global counter and sums that block's samples in order (see PT_TAKE_TASKS).
     // `sample` runs to nSamples (compat: spp; sample mode: the end of the task's block, and
     // `sample` is the absolute sample index)
-    int tile = SAMPLE ? -1 : tileOf(P, blockIdx.x), nSamples = SAMPLE ? 0 : P.spp;
+    int tile = (SAMPLE || CQ) ? -1 : tileOf(P, blockIdx.x), nSamples = SAMPLE ? 0 : P.spp;
     int col = 0, lrow = 0;
-    if constexpr (!SAMPLE) {
+    if constexpr (!SAMPLE && !CQ) {
         col = (tile % P.tiles_x) * 8 + (lane & 7);
         lrow = (tile / P.tiles_x) * 8 + (lane >> 3);
     }
-    bool valid = !SAMPLE && col < P.width && lrow < P.nrows;
+    bool valid = !SAMPLE && !CQ && col < P.width && lrow < P.nrows;
     uint32_t idx = valid ? (uint32_t)lrow * (uint32_t)P.width + (uint32_t)col : 0u;   // npix < 2^32
     const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
-    if (!SAMPLE && (int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
+    if (!SAMPLE && !CQ && (int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
     float fcol = (float)col;
     float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
@@ -1313,6 +1370,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #ifdef PT_DIAG
     uint32_t itN = 0, itL = 0, itS = 0, sPops = 0, sRedo = 0;   // scheduler diagnostics (iterations per kind)
     unsigned long long sSpecN = 0, sIdleN = 0;   // NODE steps: lanes waiting on primitives that have nodes left; lanes with no NODE work
+    unsigned long long sAvoid = 0, sHalf = 0;    // LEAF (wide): tests whose exact box misses at test time; lanes testing one primitive
+    unsigned long long sAvoidInf = 0, sParkT = 0, sParkA = 0;   // ... misses even with tmax = inf; tests / misses in parked groups
     unsigned long long cycN = 0, cycL = 0, cycS = 0, cycH = 0;   // and shader cycles per kind, loop head
     unsigned long long cycSh = 0, cycTk = 0, cycNp = 0, cycBr = 0;   // SHADE: shading, tasks, new path, ray start
 #define PT_DIAG_ADD(v, x) (v) += (x)
@@ -1342,8 +1401,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     bool active = false;
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
     uint32_t depthPaths = 0;
-    bool needTask = SAMPLE;
-    uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode: the wave's reserved tasks (uniform)
+    bool needTask = SAMPLE || CQ;
+    uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode / CQ: the wave's reserved tasks (uniform)
 
 
     // Start the closest-hit query of (o, d).  (Macros, not lambdas: a [&] closure makes the
@@ -1354,6 +1413,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         if constexpr (SAMPLE) {   /* rays per task: only frames that measure tile costs use them */ \
             if (kargs()->measureCost)                                                             \
                 __hip_atomic_fetch_add(&taskState[lane].w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+        }                                                                                         \
+        if constexpr (CQ) {   /* rays per pixel, likewise */                                     \
+            if (kargs()->measureCost)                                                             \
+                __hip_atomic_fetch_add(&pixState[lane].y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
         }                                                                                         \
         closest = __builtin_inff();                                                               \
         best = -1;                                                                                \
@@ -1453,6 +1516,71 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             }                                                                                     \
         }                                                                                         \
     } while (0)
+    // Compat mode, pixel queue (CQ): the lanes with needTask take the next pixels of the global queue,
+    // exactly as many as ask (one returning atomic; ranked in lane order by the ballot): queue slot t
+    // = pixel t % 64 of the 8x8 tile in launch slot t / 64 (longest tiles first), so a take spans at
+    // most two tiles.  No pool is reserved ahead: a pixel is a long task (all its samples), and
+    // slots held back by a wave would wait for that wave's lanes while other waves run dry.  A taken
+    // pixel's XORWOW state comes from the film (curand_init(seed, pixel, 0) or where the last frame
+    // left it).  Slots off the frame edge are skipped; lanes that find the queue exhausted stop asking.
+#define PT_TAKE_PIXELS(got)                                                                         \
+    do {                                                                                          \
+        const auto& Q_ = *kargs();                                                                \
+        for (;;) {                                                                                \
+            const uint64_t m_ = __ballot(needTask);                                               \
+            if (m_ == 0) break;                                                                   \
+            const uint32_t n_ = (uint32_t)__popcll(m_);                                           \
+            const int leader_ = __ffsll((unsigned long long)m_) - 1;                              \
+            uint32_t b_ = 0;                                                                      \
+            if (lane == leader_) b_ = atomicAdd(Q_.taskCounter, n_);                               \
+            const uint32_t base_ = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_)); \
+            const uint32_t slotA_ = base_ >> 6, slotB_ = slotA_ + 1u;                             \
+            const uint32_t nt_ = (uint32_t)Q_.ntiles;                                             \
+            const uint32_t xyA_ = slotA_ < nt_ ? ((KU32)Q_.tileXY)[__builtin_amdgcn_readfirstlane(slotA_)] : 0u; \
+            const uint32_t xyB_ = slotB_ < nt_ ? ((KU32)Q_.tileXY)[__builtin_amdgcn_readfirstlane(slotB_)] : 0u; \
+            const uint32_t k_ = (uint32_t)__popcll(m_ & ((1ull << lane) - 1ull));                 \
+            if (needTask) {                                                                       \
+                const uint32_t t_ = base_ + k_;                                                   \
+                if ((t_ >> 6) >= nt_) {                                                           \
+                    needTask = false;   /* the queue is exhausted */                               \
+                } else {                                                                          \
+                    const bool hi_ = (t_ >> 6) != slotA_;                                         \
+                    const uint32_t xy_ = hi_ ? xyB_ : xyA_, px_ = t_ & 63u;                       \
+                    const uint32_t tx_ = xy_ & 0xffffu, ty_ = xy_ >> 16;                          \
+                    const int c_ = (int)(tx_ * 8u + (px_ & 7u)), r_ = (int)(ty_ * 8u + (px_ >> 3)); \
+                    if (c_ < Q_.width && r_ < Q_.nrows) {                                           \
+                        needTask = false;                                                         \
+                        got = true;                                                               \
+                        const uint32_t i_ = (uint32_t)r_ * (uint32_t)Q_.width + (uint32_t)c_;     \
+                        pixState[lane] = make_uint4(ty_ * (uint32_t)Q_.tiles_x + tx_, 0u, i_, 0u); \
+                        fcol = (float)c_;                                                         \
+                        frow = (float)globalRowFast(r_, Q_.stripe_h, Q_.stripeShift, Q_.nparts, Q_.part); \
+                        g = Xorwow{Q_.sd[i_], Q_.s0[i_], Q_.s1[i_], Q_.s2[i_], Q_.s3[i_], Q_.s4[i_]}; \
+                        sum = f3(0.0f, 0.0f, 0.0f);                                               \
+                        sample = 0;                                                               \
+                    }                                                                             \
+                }                                                                                 \
+            }                                                                                     \
+        }                                                                                         \
+    } while (0)
+    // CQ: the lane's pixel has all its samples: its result and XORWOW state back to the film, its
+    // ray count into its tile's cost (the longest pixel of the tile: the next launch's order), and
+    // the lane asks for the next pixel.
+#define PT_FINISH_PIXEL()                                                                           \
+    do {                                                                                          \
+        const auto& Q_ = *kargs();                                                                \
+        const uint4 ps_ = pixState[lane];                                                         \
+        const uint32_t i_ = ps_.z;                                                                \
+        float* out_ = Q_.out + 3 * (size_t)i_;   /* (storePixel) */                               \
+        if (Q_.rawOut) {                                                                          \
+            out_[0] = sum.x; out_[1] = sum.y; out_[2] = sum.z;                                    \
+        } else {                                                                                  \
+            out_[0] = sqrtf(sum.x * Q_.invSpp); out_[1] = sqrtf(sum.y * Q_.invSpp); out_[2] = sqrtf(sum.z * Q_.invSpp); \
+        }                                                                                         \
+        Q_.sd[i_] = g.d; Q_.s0[i_] = g.v0; Q_.s1[i_] = g.v1; Q_.s2[i_] = g.v2; Q_.s3[i_] = g.v3; Q_.s4[i_] = g.v4; \
+        if (Q_.measureCost) atomicMax(Q_.tileCost + ps_.x, ps_.y);                                \
+        needTask = true;                                                                          \
+    } while (0)
     // Sample mode: the lane's block (= its task; ts = the task state) is complete: its sum and ray
     // count go to the pixel's accumulator (order-free integer atomics on per-pixel addresses: no
     // contention; right here -- deferring them to a later step of the loop, where fewer registers
@@ -1530,6 +1658,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             }
             needTask = false;
             waveReduceAdd(P.counters + 4, depthPaths);   // (paths counted per lane here)
+        }
+    } else if (CQ) {
+        if (P.max_depth <= 0) {   // (no bounce: every sample is its camera ray's sky colour)
+            for (;;) {
+                bool got = false;
+                PT_TAKE_PIXELS(got);
+                if (__ballot(got) == 0) break;
+                if (got) {
+                    for (; sample < nSamples; sample++) {
+                        PT_NEW_PATH();
+                        sum = add(sum, sky(d, att));
+                    }
+                    depthPaths += (uint32_t)nSamples;
+                    PT_FINISH_PIXEL();
+                }
+            }
+            needTask = false;
+            waveReduceAdd(P.counters + 4, depthPaths);
         }
     } else if (valid) {
         if (P.max_depth <= 0) {
@@ -1651,7 +1797,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                             n3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 48u, 0, 0));
                             n4 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off + 64u, 0, 0));
                         }
-                        const uint32_t hits = wideHits(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
+                        const uint32_t hits = wideHitsInst(n0, n1, n2, n3, n4, o, inv, oct & 7u, 0.001f, closest);
                         ng = (n1.x << 8) | (hits >> 24);
                         tgBase = n1.y;
                         tg = hits & 0xffffffu;
@@ -1688,11 +1834,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     ng = (n1.x << 8) | (hits >> 24);
                     tgBase = n1.y;
                     tg = hits & 0xffffffu;
+#ifdef PT_DIAG
+                    oct &= ~64u;   // (diagnostics: bit 6 marks a group that was parked)
+#endif
                     if (SPEC && tg == 0u && (oct & 48u)) {   // no new primitives: the last parked group is current again
                         oct -= 16u;
                         const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
                         tgBase = pend[(2u * c) * kWave + lane];
                         tg = pend[(2u * c + 1u) * kWave + lane];
+#ifdef PT_DIAG
+                        oct |= 64u;
+#endif
                     }
                 }
             } else if (wantNode) {
@@ -1853,6 +2005,21 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 const float4* w1 = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(k1));
                 const Prim q0{w0[0], w0[1], w0[2]}, q1{w1[0], w1[1], w1[2]};
                 bool redo = false;
+#ifdef PT_DIAG
+                {   // tests the reference would skip: the primitive's exact box misses with the
+                    // closest hit of this moment (its own leaf test, render_manager.h:107-123)
+                    const bool a0 = h0 && !refLeafBox(q0, __float_as_uint(q0.p2.w) != 0u, o, inv, 0.001f, closest).hit;
+                    const bool a1 = h1 && !refLeafBox(q1, __float_as_uint(q1.p2.w) != 0u, o, inv, 0.001f, closest).hit;
+                    sAvoid += (unsigned long long)(__popcll(__ballot(a0)) + __popcll(__ballot(a1)));
+                    sHalf += (unsigned long long)__popcll(__ballot(h0 && !h1));
+                    const bool i0 = h0 && !refLeafBox(q0, __float_as_uint(q0.p2.w) != 0u, o, inv, 0.001f, __builtin_inff()).hit;
+                    const bool i1 = h1 && !refLeafBox(q1, __float_as_uint(q1.p2.w) != 0u, o, inv, 0.001f, __builtin_inff()).hit;
+                    sAvoidInf += (unsigned long long)(__popcll(__ballot(i0)) + __popcll(__ballot(i1)));
+                    const bool pk = !INST && (oct & 64u) != 0u;
+                    sParkT += (unsigned long long)(__popcll(__ballot(pk && h0)) + __popcll(__ballot(pk && h1)));
+                    sParkA += (unsigned long long)(__popcll(__ballot(pk && a0)) + __popcll(__ballot(pk && a1)));
+                }
+#endif
                 // (instanced: no reference leaf-box rule; the hit key carries the instance)
                 const bool lb = !INST && S.nprims > 1;
                 const uint32_t kh = INST ? (oct >> 8) << kargs()->S.gBits : 0u;
@@ -1873,6 +2040,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                     const uint32_t c = SPECN == 1 ? 0u : (oct >> 4) & 3u;
                     tgBase = pend[(2u * c) * kWave + lane];
                     tg = pend[(2u * c + 1u) * kWave + lane];
+#ifdef PT_DIAG
+                    oct |= 64u;
+#endif
                 }
             } else {
             PT_DIAG_ADD(sPops, (uint32_t)nL);
@@ -1964,8 +2134,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                         }
                     } else {
                         ++sample;
-                        if (sample == nSamples) active = false;
-                        else newSample = true;
+                        if (sample == nSamples) {
+                            active = false;
+                            if constexpr (CQ) PT_FINISH_PIXEL();
+                        } else {
+                            newSample = true;
+                        }
                     }
                 }
                 newRay = true;   // bounce, next sample (newSample) or finished (reset below)
@@ -1977,6 +2151,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             if constexpr (SAMPLE) {   // idle lanes take new tasks and start their first path
                 bool got = false;
                 PT_TAKE_TASKS(got);
+                if (got) {
+                    active = true;
+                    newRay = newSample = true;
+                }
+            } else if constexpr (CQ) {   // idle lanes take new pixels and start their first sample
+                bool got = false;
+                PT_TAKE_PIXELS(got);
                 if (got) {
                     active = true;
                     newRay = newSample = true;
@@ -2007,14 +2188,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }
 #endif
     }
-    if constexpr (!SAMPLE) {   // (sample mode: every task wrote its block sum when it closed)
+    if constexpr (!SAMPLE && !CQ) {   // (sample mode / CQ: every task wrote its result when it ended)
         if (valid) {
             storePixel(P, idx, sum);
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
         }
     }
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
-    if (!SAMPLE && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
+    if (!SAMPLE && !CQ && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
     if constexpr (SAMPLE) {   // max_depth <= 0: paths counted per lane
 
     }
@@ -2047,6 +2228,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         atomicAdd(P.counters + 20, (unsigned long long)sRedo);
         atomicAdd(P.counters + 21, sSpecN);
         atomicAdd(P.counters + 22, sIdleN);
+        atomicAdd(P.counters + 23, sAvoid);
+        atomicAdd(P.counters + 25, sHalf);
+        atomicAdd(P.counters + 26, sAvoidInf);
+        atomicAdd(P.counters + 27, sParkT);
+        atomicAdd(P.counters + 28, sParkA);
 #endif
     }
 }
@@ -2054,6 +2240,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK
+#undef PT_TAKE_PIXELS
+#undef PT_FINISH_PIXEL
 #undef PT_CLOSE_BLOCK
 #undef PT_DIAG_ADD
 
@@ -2068,12 +2256,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 namespace pt {
 int launchCompatWide(int stack, const void* params, hipStream_t st) {
     const RenderParams& P = *static_cast<const RenderParams*>(params);
+    const int grid = PT_COMPAT_QUEUE ? P.nwaves : P.ntiles;   // persistent waves with the pixel queue
     switch (stack) {
-        case 8: renderKernelWF<8, false, true><<<P.ntiles, kWave, 0, st>>>(P); break;
-        case 16: renderKernelWF<16, false, true><<<P.ntiles, kWave, 0, st>>>(P); break;
-        case 24: renderKernelWF<24, false, true><<<P.ntiles, kWave, 0, st>>>(P); break;
+        case 8: renderKernelWF<8, false, true><<<grid, kWave, 0, st>>>(P); break;
+        case 16: renderKernelWF<16, false, true><<<grid, kWave, 0, st>>>(P); break;
+        case 24: renderKernelWF<24, false, true><<<grid, kWave, 0, st>>>(P); break;
         default: return -1;
     }
+    return 0;
+}
+int compatWideWavesPerCU(int stack, int& n) {
+    const void* k = stack == 8 ? reinterpret_cast<const void*>(&renderKernelWF<8, false, true>)
+                  : stack == 16 ? reinterpret_cast<const void*>(&renderKernelWF<16, false, true>)
+                  : stack == 24 ? reinterpret_cast<const void*>(&renderKernelWF<24, false, true>) : nullptr;
+    if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWave, 0) != hipSuccess) return -1;
     return 0;
 }
 }  // namespace pt
@@ -2289,7 +2485,8 @@ __global__ __launch_bounds__(kWave) void traceKernelWide(DevScene S, const pt_ra
                 tg = 0u;
                 continue;
             }
-            const uint32_t h = wideHits<!INST && PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest);
+            const uint32_t h = INST ? wideHitsInst(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest)
+                                    : wideHits<PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest);
             ng = (n1.x << 8) | (h >> 24);
             tgBase = n1.y;
             tg = h & 0xffffffu;
@@ -2576,7 +2773,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PT_TRACE_
                         tg = 0u;
                     }
                 } else {
-                    const uint32_t h = wideHits<!INST && PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest);
+                    const uint32_t h = INST ? wideHitsInst(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest)
+                                            : wideHits<PT_WIDE_MIX != 0>(n0, n1, n2, n3, n4, o, inv, oct, tminI, closest);
                     ng = (n1.x << 8) | (h >> 24);
                     tgBase = n1.y;
                     tg = h & 0xffffffu;
@@ -3528,7 +3726,7 @@ template <int S>
 void launchRenderWide(const RenderParams& P, hipStream_t st) {
     if (P.S.winst) {   // an instanced scene's two-level tree
         if (P.pixAcc) renderKernelWF<S, true, true, true><<<P.nwaves, kWave, 0, st>>>(P);
-        else renderKernelWF<S, false, true, true><<<P.ntiles, kWave, 0, st>>>(P);
+        else renderKernelWF<S, false, true, true><<<PT_COMPAT_QUEUE ? P.nwaves : P.ntiles, kWave, 0, st>>>(P);
         return;
     }
     if (P.pixAcc) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
@@ -3539,26 +3737,29 @@ void launchRender(const RenderParams& P, hipStream_t st) {
     if (P.kernel == PT_KERNEL_WAVEFRONT && P.pixAcc)
         renderKernelWF<S, true, false><<<P.nwaves, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT)
-        renderKernelWF<S, false, false><<<P.ntiles, kWave, 0, st>>>(P);
+        renderKernelWF<S, false, false><<<PT_COMPAT_QUEUE ? P.nwaves : P.ntiles, kWave, 0, st>>>(P);
     else if (P.pixAcc) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
-template <int S, bool WIDE, bool INST = false>
+template <int S, bool WIDE, bool INST = false, bool SAMPLE = true>
 int wavesPerCU(int& n) {
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&renderKernelWF<S, true, WIDE, INST>),
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&renderKernelWF<S, SAMPLE, WIDE, INST>),
                                                          kWave, 0));
     return PT_OK;
 }
-int persistentWavesPerCU(int stack, int kernel, int& n, bool inst = false) {
+// Persistent waves per CU of the render kernel a launch runs (sample mode, or compat mode with the
+// pixel queue): its occupancy.  The compat wide kernels live in pt_compat.hip's translation unit.
+int persistentWavesPerCU(int stack, int kernel, int& n, bool inst, bool sample) {
     if (kernel == PT_KERNEL_WIDE && inst) {
         switch (stack) {
-            case 8: return wavesPerCU<8, true, true>(n);
-            case 16: return wavesPerCU<16, true, true>(n);
-            case 24: return wavesPerCU<24, true, true>(n);
+            case 8: return sample ? wavesPerCU<8, true, true>(n) : wavesPerCU<8, true, true, false>(n);
+            case 16: return sample ? wavesPerCU<16, true, true>(n) : wavesPerCU<16, true, true, false>(n);
+            case 24: return sample ? wavesPerCU<24, true, true>(n) : wavesPerCU<24, true, true, false>(n);
             default: return fail(PT_ERR_STATE, "unsupported instanced BVH depth");
         }
     }
     if (kernel == PT_KERNEL_WIDE) {
+        if (!sample) return pt::compatWideWavesPerCU(stack, n) ? fail(PT_ERR_STATE, "unsupported wide BVH depth") : PT_OK;
         switch (stack) {
             case 8: return wavesPerCU<8, true>(n);
             case 16: return wavesPerCU<16, true>(n);
@@ -3567,14 +3768,14 @@ int persistentWavesPerCU(int stack, int kernel, int& n, bool inst = false) {
         }
     }
     switch (stack) {
-        case 16: return wavesPerCU<16, false>(n);
+        case 16: return sample ? wavesPerCU<16, false>(n) : wavesPerCU<16, false, false, false>(n);
 #if PT_STACK24
-        case 24: return wavesPerCU<24, false>(n);
+        case 24: return sample ? wavesPerCU<24, false>(n) : wavesPerCU<24, false, false, false>(n);
 #endif
-        case 32: return wavesPerCU<32, false>(n);
-        case 48: return wavesPerCU<48, false>(n);
-        case 64: return wavesPerCU<64, false>(n);
-        case 80: return wavesPerCU<80, false>(n);
+        case 32: return sample ? wavesPerCU<32, false>(n) : wavesPerCU<32, false, false, false>(n);
+        case 48: return sample ? wavesPerCU<48, false>(n) : wavesPerCU<48, false, false, false>(n);
+        case 64: return sample ? wavesPerCU<64, false>(n) : wavesPerCU<64, false, false, false>(n);
+        case 80: return sample ? wavesPerCU<80, false>(n) : wavesPerCU<80, false, false, false>(n);
         default: return fail(PT_ERR_STATE, "unsupported BVH depth");
     }
 }
@@ -3752,6 +3953,14 @@ void printIterStats(const unsigned long long* c, bool wide) {
         std::fprintf(stderr, "[pt] wide queries repeated in the reference order: %llu (lanes x steps); NODE steps: "
                      "lanes waiting on primitives with nodes left %.1f, lanes without NODE work %.1f\n", c[20],
                      (double)c[21] / std::max(1ull, c[8]), (double)c[22] / std::max(1ull, c[8]));
+    if (wide && c[9] > 0)
+        std::fprintf(stderr, "[pt] LEAF: primitive tests whose exact box misses at test time %llu of %llu (%.3f); "
+                     "lanes testing one primitive per step %.1f\n", c[23], c[3] + c[2], (double)c[23] / std::max(1ull, c[2] + c[3]),
+                     (double)c[25] / std::max(1ull, c[9]));
+    if (wide && c[9] > 0)
+        std::fprintf(stderr, "[pt] LEAF: exact box misses even with tmax = inf %llu (%.3f of tests); tests in groups that "
+                     "were parked %llu (%.3f), their misses %llu\n", c[26], (double)c[26] / std::max(1ull, c[2] + c[3]),
+                     c[27], (double)c[27] / std::max(1ull, c[2] + c[3]), c[28]);
     if (c[15] > 0)
         std::fprintf(stderr, "[pt] loop head (choice of the step kind) cycles/iteration %.0f\n",
                      (double)c[15] / std::max(1ull, c[8] + c[9] + c[10]));
@@ -4393,6 +4602,45 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     }
     const bool lpt = !(opts && (opts->flags & PT_RENDER_IDENTITY_ORDER));
     const bool sample = rng == PT_RNG_SAMPLE && np > 0 && P.ntiles > 0;
+    // compat mode, pixel queue (renderKernelWF, PT_COMPAT_QUEUE): persistent waves take pixels
+    const bool cq = PT_COMPAT_QUEUE && !sample && kernel != PT_KERNEL_SIMPLE && np > 0 && P.ntiles > 0;
+    if (!f->cus) {
+        if (hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device) != hipSuccess)
+            f->cus = 256;
+        f->cus = std::max(f->cus, 1);
+    }
+    // persistent waves (sample mode, CQ): exactly the waves that fit at once -- the kernel's
+    // occupancy per CU, which the LDS stack caps on deep trees.  Queried once per (device, kernel
+    // instantiation) and process.
+    auto perCUFor = [&](int& perCU) -> int {
+        static std::atomic<int> cached[16][2][2][2][3];   // [device][sample][instanced][wide][stack 8, 16, 24]
+        const bool small = stack <= 24 && stack % 8 == 0 && f->device >= 0 && f->device < 16;
+        std::atomic<int>* c = small ? &cached[f->device][sample ? 1 : 0][s->instanced ? 1 : 0]
+                                             [kernel == PT_KERNEL_WIDE ? 1 : 0][stack / 8 - 1] : nullptr;
+        const int known = c ? c->load(std::memory_order_relaxed) : 0;
+        if (known > 0) {
+            perCU = known;
+            return PT_OK;
+        }
+        if (int r = persistentWavesPerCU(stack, kernel, perCU, s->instanced, sample)) return r;
+        if (c) c->store(perCU, std::memory_order_relaxed);
+        return PT_OK;
+    };
+    if (cq) {
+        P.ntasks = (uint32_t)P.ntiles * 64u;   // queue slots: tile slot x 64 pixels
+        if (!f->taskCounter.p && (rc = devAlloc(f->taskCounter, 64))) return rc;
+        HIP_TRY(hipMemsetAsync(f->taskCounter.p, 0, 4, st));
+        P.taskCounter = f->taskCounter.as<unsigned>();
+        int perCU = 0;
+        if ((rc = perCUFor(perCU))) return rc;
+        P.nwaves = (int)std::min<uint64_t>((uint64_t)f->cus * (uint64_t)std::max(1, perCU) * (uint64_t)envInt("PT_CQ_WAVES_MULT", 1),
+                                           (uint64_t)P.ntiles);
+        if (std::getenv("PT_ITER_STATS"))
+            std::fprintf(stderr, "[pt] compat pixel queue: persistent waves %d (%d per CU, stack %d)\n", P.nwaves, perCU, stack);
+        // tile costs (the rays of the tile's longest pixel, atomicMax per pixel) on every launch
+        P.measureCost = lpt ? 1 : 0;
+        if (P.measureCost) HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));
+    }
     if (sample) {
         if (f->width >= 65536 || f->nrows >= 65536)
             return fail(PT_ERR_INVALID, "sample mode: frame width and rows must be < 65536");
@@ -4414,26 +4662,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if (!f->taskCounter.p && (rc = devAlloc(f->taskCounter, 64))) return rc;
         HIP_TRY(hipMemsetAsync(f->taskCounter.p, 0, 4, st));
         P.taskCounter = f->taskCounter.as<unsigned>();
-        if (!f->cus) {
-            if (hipDeviceGetAttribute(&f->cus, hipDeviceAttributeMultiprocessorCount, f->device) != hipSuccess)
-                f->cus = 256;
-            f->cus = std::max(f->cus, 1);
-        }
-        // persistent: exactly the waves that fit at once (the kernel's occupancy per CU, which
-        // the LDS stack caps below PT_WAVES_PER_EU per SIMD on deep trees)
         int perCU = 0;
-        {   // (the occupancy of a kernel instantiation does not change: queried once per process)
-            static std::atomic<int> cached[2][2][3];   // [instanced][wide][stack 8, 16, 24]
-            const bool small = stack <= 24 && stack % 8 == 0;
-            std::atomic<int>* c = small ? &cached[s->instanced ? 1 : 0][kernel == PT_KERNEL_WIDE ? 1 : 0][stack / 8 - 1] : nullptr;
-            const int known = c ? c->load(std::memory_order_relaxed) : 0;
-            if (known > 0) {
-                perCU = known;
-            } else {
-                if ((rc = persistentWavesPerCU(stack, kernel, perCU, s->instanced))) return rc;
-                if (c) c->store(perCU, std::memory_order_relaxed);
-            }
-        }
+        if ((rc = perCUFor(perCU))) return rc;
         const uint64_t full = (uint64_t)f->cus * (uint64_t)std::max(1, perCU);
         P.nwaves = (int)std::min<uint64_t>(full, (ntasks + 63) / 64);
         if (std::getenv("PT_ITER_STATS"))
@@ -4448,7 +4678,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     // Deep trees: stack entries beyond kLdsStack live in memory, per wave slot (persistent wave or
     // compat tile) and lane
     if (kernel == PT_KERNEL_WAVEFRONT && stack > PT_LDS_STACK && P.ntiles > 0) {
-        const size_t slots = sample ? (size_t)P.nwaves : (size_t)P.ntiles;
+        const size_t slots = (sample || cq) ? (size_t)P.nwaves : (size_t)P.ntiles;
         if ((rc = devReserve(f->stackSpill, slots * kWave * (size_t)(stack - PT_LDS_STACK) * 4))) return rc;
         P.stackSpill = f->stackSpill.as<uint32_t>();
     }
@@ -4472,8 +4702,8 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.tileOrder = (lpt && f->haveOrder) ? f->tileOrder.as<int>() : nullptr;
     P.tileXY = nullptr;
     P.nblocksShift = -1;
-    if (sample) {   // the launch order decoded per slot (tileXYKernel; the ordered table follows each sort)
-        P.nblocksShift = (P.ngroups & (P.ngroups - 1)) == 0 ? __builtin_ctz((unsigned)P.ngroups) : -1;
+    if (sample || cq) {   // the launch order decoded per slot (tileXYKernel; the ordered table follows each sort)
+        if (sample) P.nblocksShift = (P.ngroups & (P.ngroups - 1)) == 0 ? __builtin_ctz((unsigned)P.ngroups) : -1;
         if (!P.tileOrder && !f->haveXYId) {
             tileXYKernel<<<(unsigned)((ntl + 255) / 256), 256, 0, st>>>(nullptr, (int)ntl, P.tiles_x, f->tileXYId.as<uint32_t>());
             HIP_TRY(hipGetLastError());
@@ -4481,11 +4711,11 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         }
         P.tileXY = P.tileOrder ? f->tileXY.as<uint32_t>() : f->tileXYId.as<uint32_t>();
     }
-    P.prioTiles = (P.tileOrder && !sample) ? envInt("PT_PRIO_TILES", 1024) : 0;
+    P.prioTiles = (P.tileOrder && !sample && !cq) ? envInt("PT_PRIO_TILES", 1024) : 0;
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
-    const size_t nwaves = sample ? (size_t)P.nwaves : ntl;   // = grid size
+    const size_t nwaves = (sample || (cq && kernel != PT_KERNEL_SIMPLE)) ? (size_t)P.nwaves : ntl;   // = grid size
     if (timesPath && *timesPath && kernel != PT_KERNEL_SIMPLE) {
         if ((rc = devAlloc(dtimes, nwaves * 24))) return rc;
         HIP_TRY(hipMemsetAsync(dtimes.p, 0, nwaves * 24, st));

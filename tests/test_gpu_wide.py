@@ -333,8 +333,9 @@ def test_wide_render_far_camera(pt, orc, gpu, wb):
 def test_wide_trace_near_axis_directions(pt, orc, gpu, wb, name):
     """The MIX plane arithmetic (wideHits<MIX>: fp16-denormal planes, scale s * 2^24 * inv) is exact
     while |inv| <= DevScene::mixLim; rays with a finite |1/d| component beyond it take the
-    reference-order query (mixUnsafe), and exactly zero components (|inv| = inf) stay on the wide
-    path.  Axis-parallel and nearly axis-parallel rays (components 0, +-2^-100, +-2^-126, denormal)
+    reference-order query (mixUnsafe), and so do rays with an exactly zero component (|inv| = inf:
+    the decomposed planes would be NaN; since round 4, node visits guarded by
+    test_gpu_zero_axis.py).  Axis-parallel and nearly axis-parallel rays (components 0, +-2^-100, +-2^-126, denormal)
     through the Cornell box's axis-aligned walls, from inside the box and aimed at vertices, keep
     the reference's hits bit for bit."""
     p = pt.Preset(name, 32, 32)

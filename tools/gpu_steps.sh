@@ -9,6 +9,7 @@ status=0
 for spec in "$@"; do
     name=${spec%%|*}; rest=${spec#*|}; secs=${rest%%|*}; cmd=${rest#*|}
     echo "== $name ($secs s): $cmd"
+    mkdir -p "$(dirname "gpurun_out/$name.log")"
     timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
     rc=$?
     echo "== $name rc=$rc"
