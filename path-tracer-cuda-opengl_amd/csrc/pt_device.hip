@@ -983,6 +983,8 @@ struct RenderParams {
     int camFar;                               // wide: the camera lies beyond the wide boxes' margin (wideFar)
     int rawOut;                               // compat: store the raw sample sum (resolveKernel follows)
     int stripeShift, blockShift;              // log2(stripe_h), log2(block) when powers of two, else -1
+    int splitTiles, splitWays;                // compat: the longest tiles run as splitWays waves each
+    int compatGrid;                           // compat (tile waves): ntiles + splitTiles * (splitWays - 1)
 };
 
 // Sample mode: a block's fp32 sum as a 32.32 fixed-point integer (truncated toward zero; NaN -> 0,
@@ -1228,6 +1230,12 @@ constexpr int kTaskBlocks = PT_TASK_BLOCKS;   // sample mode: summation blocks p
 #endif
 template <int STACK, bool SAMPLE, bool WIDE>
 constexpr int kLdsStack = (!WIDE && STACK > PT_LDS_STACK) ? PT_LDS_STACK : STACK;
+#ifndef PT_AB_NO_SPLIT
+#define PT_AB_NO_SPLIT 0   // (A/B only: compile the compat split-tile prologue out)
+#endif
+#ifndef PT_AB_COST_STORE
+#define PT_AB_COST_STORE 0   // (A/B only: compat tile costs stored, not atomicMax'ed -- wrong with split tiles)
+#endif
 #ifndef PT_COMPAT_QUEUE
 #define PT_COMPAT_QUEUE 0   // compat mode: persistent waves take pixels from a queue (else one wave per tile; 1 measured slower)
 #endif
@@ -1348,16 +1356,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // block) from a global counter and sums that block's samples in order (see PT_TAKE_TASKS).
     // `sample` runs to nSamples (compat: spp; sample mode: the end of the task's block, and
     // `sample` is the absolute sample index)
-    int tile = (SAMPLE || CQ) ? -1 : tileOf(P, blockIdx.x), nSamples = SAMPLE ? 0 : P.spp;
+    // Compat mode, split tiles: the first splitTiles tiles of the launch order (the longest: their
+    // pixels' sequential chains are the frame's critical path) run as splitWays waves each, one slice
+    // of 64 / splitWays pixels per wave (the other lanes idle), so a critical pixel shares its wave's
+    // steps with fewer other pixels and its chain advances in more of them.
+    int bidT = (int)blockIdx.x, slice = -1;
+    if constexpr (!SAMPLE && !CQ && !PT_AB_NO_SPLIT) {
+        const int ks = P.splitTiles * P.splitWays;   // (uniform)
+        if (bidT < ks) { slice = bidT % P.splitWays; bidT /= P.splitWays; }
+        else bidT -= ks - P.splitTiles;
+    }
+    int tile = (SAMPLE || CQ) ? -1 : tileOf(P, bidT), nSamples = SAMPLE ? 0 : P.spp;
     int col = 0, lrow = 0;
     if constexpr (!SAMPLE && !CQ) {
         col = (tile % P.tiles_x) * 8 + (lane & 7);
         lrow = (tile / P.tiles_x) * 8 + (lane >> 3);
     }
-    bool valid = !SAMPLE && !CQ && col < P.width && lrow < P.nrows;
+    bool valid = !SAMPLE && !CQ && col < P.width && lrow < P.nrows && (slice < 0 || (lane * P.splitWays) / kWave == slice);
     uint32_t idx = valid ? (uint32_t)lrow * (uint32_t)P.width + (uint32_t)col : 0u;   // npix < 2^32
     const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
-    if (!SAMPLE && !CQ && (int)blockIdx.x < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
+    if (!SAMPLE && !CQ && bidT < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
     float fcol = (float)col;
     float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
@@ -2195,7 +2213,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         }
     }
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
+#if PT_AB_COST_STORE
     if (!SAMPLE && !CQ && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
+#else
+    if (!SAMPLE && !CQ && lane == 0) atomicMax(P.tileCost + tile, (unsigned)min(tEnd - tStart, 0xffffffffull));   // (split tiles: several waves)
+#endif
     if constexpr (SAMPLE) {   // max_depth <= 0: paths counted per lane
 
     }
@@ -2256,7 +2278,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
 namespace pt {
 int launchCompatWide(int stack, const void* params, hipStream_t st) {
     const RenderParams& P = *static_cast<const RenderParams*>(params);
-    const int grid = PT_COMPAT_QUEUE ? P.nwaves : P.ntiles;   // persistent waves with the pixel queue
+    const int grid = PT_COMPAT_QUEUE ? P.nwaves : P.compatGrid;   // persistent waves with the pixel queue
     switch (stack) {
         case 8: renderKernelWF<8, false, true><<<grid, kWave, 0, st>>>(P); break;
         case 16: renderKernelWF<16, false, true><<<grid, kWave, 0, st>>>(P); break;
@@ -3190,6 +3212,15 @@ int envInt(const char* name, int dflt) {
     if (x < 1) return dflt;   // "0": the default
     return x > 64 ? 64 : x;
 }
+// A count knob: any value >= 0 (0 is zero, not the default); unset or unparsable: the default.
+int envCount(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    char* end = nullptr;
+    const long x = std::strtol(v, &end, 10);
+    if (end == v || x < 0) return dflt;
+    return (int)std::min<long>(x, 1L << 30);
+}
 
 // Events of a synchronous device step; on an early return (ok still false) the stream's queued
 // work is waited for before the caller can free or reuse what it reads.
@@ -3726,7 +3757,7 @@ template <int S>
 void launchRenderWide(const RenderParams& P, hipStream_t st) {
     if (P.S.winst) {   // an instanced scene's two-level tree
         if (P.pixAcc) renderKernelWF<S, true, true, true><<<P.nwaves, kWave, 0, st>>>(P);
-        else renderKernelWF<S, false, true, true><<<PT_COMPAT_QUEUE ? P.nwaves : P.ntiles, kWave, 0, st>>>(P);
+        else renderKernelWF<S, false, true, true><<<PT_COMPAT_QUEUE ? P.nwaves : P.compatGrid, kWave, 0, st>>>(P);
         return;
     }
     if (P.pixAcc) renderKernelWF<S, true, true><<<P.nwaves, kWave, 0, st>>>(P);
@@ -3737,7 +3768,7 @@ void launchRender(const RenderParams& P, hipStream_t st) {
     if (P.kernel == PT_KERNEL_WAVEFRONT && P.pixAcc)
         renderKernelWF<S, true, false><<<P.nwaves, kWave, 0, st>>>(P);
     else if (P.kernel == PT_KERNEL_WAVEFRONT)
-        renderKernelWF<S, false, false><<<PT_COMPAT_QUEUE ? P.nwaves : P.ntiles, kWave, 0, st>>>(P);
+        renderKernelWF<S, false, false><<<PT_COMPAT_QUEUE ? P.nwaves : P.compatGrid, kWave, 0, st>>>(P);
     else if (P.pixAcc) renderKernel<S, true><<<P.ntiles, kWave, 0, st>>>(P);
     else renderKernel<S, false><<<P.ntiles, kWave, 0, st>>>(P);
 }
@@ -4626,6 +4657,12 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if (c) c->store(perCU, std::memory_order_relaxed);
         return PT_OK;
     };
+    // compat tile waves: the longest tiles of the launch order split into splitWays waves (renderKernelWF)
+    P.splitWays = std::max(1, std::min(8, envCount("PT_SPLIT_WAYS", 2)));
+    P.splitTiles = (lpt && f->haveOrder && !sample && !cq && kernel != PT_KERNEL_SIMPLE)
+                       ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", 128))) : 0;
+    if (P.splitWays == 1) P.splitTiles = 0;
+    P.compatGrid = P.ntiles + P.splitTiles * (P.splitWays - 1);
     if (cq) {
         P.ntasks = (uint32_t)P.ntiles * 64u;   // queue slots: tile slot x 64 pixels
         if (!f->taskCounter.p && (rc = devAlloc(f->taskCounter, 64))) return rc;
@@ -4678,7 +4715,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     // Deep trees: stack entries beyond kLdsStack live in memory, per wave slot (persistent wave or
     // compat tile) and lane
     if (kernel == PT_KERNEL_WAVEFRONT && stack > PT_LDS_STACK && P.ntiles > 0) {
-        const size_t slots = (sample || cq) ? (size_t)P.nwaves : (size_t)P.ntiles;
+        const size_t slots = (sample || cq) ? (size_t)P.nwaves : (size_t)P.compatGrid;
         if ((rc = devReserve(f->stackSpill, slots * kWave * (size_t)(stack - PT_LDS_STACK) * 4))) return rc;
         P.stackSpill = f->stackSpill.as<uint32_t>();
     }
@@ -4711,11 +4748,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         }
         P.tileXY = P.tileOrder ? f->tileXY.as<uint32_t>() : f->tileXYId.as<uint32_t>();
     }
-    P.prioTiles = (P.tileOrder && !sample && !cq) ? envInt("PT_PRIO_TILES", 1024) : 0;
+    P.prioTiles = (P.tileOrder && !sample && !cq) ? envCount("PT_PRIO_TILES", 1024) : 0;
+    if (!sample && !cq && kernel != PT_KERNEL_SIMPLE && P.ntiles > 0)   // (tile costs: atomicMax of the tile's waves)
+        HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));
     DevBuf dtimes;
     const char* timesPath = std::getenv("PT_WAVE_TIMES");   // diagnostic: per-wave timestamps
     P.waveTimes = nullptr;
-    const size_t nwaves = (sample || (cq && kernel != PT_KERNEL_SIMPLE)) ? (size_t)P.nwaves : ntl;   // = grid size
+    const size_t nwaves = (sample || (cq && kernel != PT_KERNEL_SIMPLE)) ? (size_t)P.nwaves
+                        : (kernel != PT_KERNEL_SIMPLE ? (size_t)std::max(1, P.compatGrid) : ntl);   // = grid size
     if (timesPath && *timesPath && kernel != PT_KERNEL_SIMPLE) {
         if ((rc = devAlloc(dtimes, nwaves * 24))) return rc;
         HIP_TRY(hipMemsetAsync(dtimes.p, 0, nwaves * 24, st));
@@ -4760,6 +4800,21 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
                                                                    f->tileXY.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         f->haveOrder = true;
+        if (std::getenv("PT_CHECK_ORDER")) {   // diagnostic: the launch order must be a permutation of the tiles
+            std::vector<uint32_t> ord(ntl), cst(ntl);
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipMemcpy(ord.data(), f->tileOrder.p, ntl * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(cst.data(), f->tileCost.p, ntl * 4, hipMemcpyDeviceToHost));
+            std::vector<uint8_t> seen(ntl, 0);
+            size_t dup = 0, bad = 0, unsorted = 0;
+            for (size_t k = 0; k < ntl; k++) {
+                if (ord[k] >= ntl) { bad++; continue; }
+                if (seen[ord[k]]++) dup++;
+                if (k && ord[k - 1] < ntl && cst[ord[k - 1]] < cst[ord[k]]) unsorted++;
+            }
+            std::fprintf(stderr, "[pt] tile order check: %zu tiles, %zu out of range, %zu duplicates, %zu unsorted pairs\n",
+                         ntl, bad, dup, unsorted);
+        }
     }
     if (P.waveTimes) {
         HIP_TRY(hipStreamSynchronize(st));

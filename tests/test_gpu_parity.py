@@ -519,3 +519,31 @@ def test_device_build_c5_faster_than_host_keys(pt, gpu):
     assert_nodes_equal(s.download_bvh(), a)
     print(f"C5 LBVH build: device {t_dev * 1e3:.1f} ms, host keys {t_host * 1e3:.1f} ms")
     assert t_dev < t_host
+
+
+@pytest.mark.parametrize("ways", [2, 4, 8])
+@pytest.mark.parametrize("kname", ["wide", "wavefront"])
+def test_compat_split_tiles_bit_exact(pt, orc, gpu, monkeypatch, kname, ways):
+    """Compat mode's split tiles (PT_SPLIT_TILES / PT_SPLIT_WAYS: the longest tiles of the launch
+    order run as `ways` waves of 64 / ways pixels each): launches after the first have a longest-
+    first order and split; every launch's frame and advanced RNG streams equal the oracle's, with
+    all tiles split and with only some (the frame's pixels rendered exactly once)."""
+    monkeypatch.setenv("PT_RENDER_KERNEL", kname)
+    monkeypatch.setenv("PT_SPLIT_WAYS", str(ways))
+    w, h, spp, depth = 72, 40, 3, 50
+    p = pt.Preset("bunny_cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    f = pt.Film(w, h, 4, device=gpu)
+    ref_states = orc.film_states(4, w, f.rows)   # (advanced by the render below)
+    ref, rst = orc.render(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, f.rows, spp, depth,
+                          ref_states, nthreads=8)
+    ntiles = ((w + 7) // 8) * ((h + 7) // 8)
+    for split in (str(ntiles), "7", "0"):
+        monkeypatch.setenv("PT_SPLIT_TILES", split)
+        for _ in range(2):   # (the first launch of a film has no order yet; later ones split)
+            f.reset()
+            rgb, st = pt.render(s, f, p.camera, spp, depth)
+            np.testing.assert_array_equal(bits(rgb), bits(ref))
+            assert st.rays == rst.rays and st.paths == w * h * spp
+            np.testing.assert_array_equal(f.get_rng(), ref_states)

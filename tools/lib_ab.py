@@ -26,7 +26,7 @@ def main():
         for name, lib, chunk, envs in libs:
             env = dict(os.environ, PT_LIB=os.path.join(REPO, lib), REPEAT=os.environ.get("REPEAT", "2"))
             env.update(dict(e.split("=", 1) for e in envs.split(",") if e))
-            out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "one_frame.py"), cfg, spp, "sample", chunk],
+            out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "one_frame.py"), cfg, spp, os.environ.get("RNG", "sample"), chunk],
                                  env=env, capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(name, "failed", out.stderr[-800:], flush=True)
