@@ -59,6 +59,21 @@ constexpr int kWave = 64;
 #ifndef PT_AB_NO_ATOMICS
 #define PT_AB_NO_ATOMICS 0
 #endif
+// Time-only A/B switches (wrong images; DESIGN.md section 11's VALU budget): the Lambertian
+// rejection loop cut to its first trial; the sample-mode Philox seeding replaced by a two-multiply
+// hash; the ray start without its MIX-range check and with a bare v_rcp_f32.
+#ifndef PT_FIXED_SMALL
+#define PT_FIXED_SMALL 1   // sample mode: blockFixedSmall when every finishing lane's sums are in [0, 2^24)
+#endif
+#ifndef PT_AB_ONE_TRIAL
+#define PT_AB_ONE_TRIAL 0
+#endif
+#ifndef PT_AB_CHEAP_SEED
+#define PT_AB_CHEAP_SEED 0
+#endif
+#ifndef PT_AB_CHEAP_START
+#define PT_AB_CHEAP_START 0
+#endif
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kSphereBit = 0x40000000u;
 constexpr uint32_t kPrimMask = 0x3fffffffu;
@@ -151,6 +166,12 @@ struct Xorwow {
 // then cost a few shifts each (the reference's generator family, curand_uniform mapping).
 // Any sample of any pixel starts anywhere, in one block of work.
 __device__ __forceinline__ Xorwow sampleStream(uint32_t k0, uint32_t k1, uint32_t sample, uint32_t pixel) {
+#if PT_AB_CHEAP_SEED   // (A/B timing only: no Philox rounds)
+    {
+        const uint32_t a = (sample ^ k0) * 0x9E3779B9u, b = (pixel ^ k1) * 0x85EBCA6Bu;
+        return Xorwow{a, a ^ b, b + 0x6C078965u, a + b, (a ^ 0x2545F491u) | 1u, b ^ 0x53414D50u};
+    }
+#endif
     uint32_t c0 = sample, c1 = pixel, c2 = 0u, c3 = 0x53414D50u;
 #pragma unroll 2   // (pairs of rounds: no register moves; a full unroll raises the camera-ray site's pressure)
     for (int r = 0; r < 10; r++) {
@@ -817,7 +838,7 @@ __device__ __forceinline__ float3 onUnitSphere(G& g) {
         const float cz = g.centered2();
         res = f3(a, b, cz);
         norm = len2(res);
-    } while (norm >= 1.0f);
+    } while (!PT_AB_ONE_TRIAL && norm >= 1.0f);
     return divs(res, sqrtf(norm));
 }
 template <class G>
@@ -987,19 +1008,7 @@ struct RenderParams {
     int compatGrid;                           // compat (tile waves): ntiles + splitTiles * (splitWays - 1)
 };
 
-// Sample mode: a block's fp32 sum as a 32.32 fixed-point integer (truncated toward zero; NaN -> 0,
-// saturated at +-2^62), and back (oracle/pt_oracle.cpp blockFixed / fixedToFloat, same roundings).
-// (Truncation done as two 32-bit halves of |p|: a * 2^-32 and a - hi * 2^32 are exact, hi has at
-// most 24 significant bits; fewer registers than the generic float -> int64 conversion.)
-__device__ __forceinline__ unsigned long long blockFixed(float x) {
-    const float p = x * 4294967296.0f;   // exact: a power-of-two scale
-    const float a = p == p ? fminf(fabsf(p), 0x1p62f) : 0.0f;
-    const uint32_t hi = (uint32_t)(a * 0x1p-32f);
-    const uint32_t lo = (uint32_t)__builtin_fmaf((float)hi, -0x1p32f, a);
-    const unsigned long long u = ((unsigned long long)hi << 32) | lo;
-    return p < 0.0f ? 0ull - u : u;
-}
-__device__ __forceinline__ float fixedToFloat(unsigned long long a) { return (float)((double)(long long)a * 0x1p-32); }
+// (blockFixed, blockFixedSmall, fixedToFloat: pt_math.hpp)
 // One finished (pixel, block) task: its sum added to the pixel's accumulator, and -- on frames
 // that measure tile costs (`cost`: the input of the next launches' longest-first order) -- its ray
 // count; no-return atomics (device scope: 4 of them per task cost 5 % of a C3 frame, so the ray
@@ -1014,9 +1023,19 @@ __device__ __forceinline__ void addBlock(unsigned long long* acc, float3 sum, ui
 #if PT_AB_NO_ATOMICS
     return;
 #endif
-    __hip_atomic_fetch_add(acc + 0, blockFixed(sum.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(acc + 1, blockFixed(sum.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(acc + 2, blockFixed(sum.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the common case -- every finishing lane's three sums in [0, 2^24), NaN excluded by the >= 0
+    // tests -- takes blockFixedSmall (a wave-uniform branch on the ballot)
+    const bool small = sum.x >= 0.0f && sum.y >= 0.0f && sum.z >= 0.0f &&
+                       fmaxf(fmaxf(sum.x, sum.y), sum.z) < 16777216.0f;
+    unsigned long long fx, fy, fz;
+    if (PT_FIXED_SMALL && __ballot(!small) == 0) {
+        fx = blockFixedSmall(sum.x); fy = blockFixedSmall(sum.y); fz = blockFixedSmall(sum.z);
+    } else {
+        fx = blockFixed(sum.x); fy = blockFixed(sum.y); fz = blockFixed(sum.z);
+    }
+    __hip_atomic_fetch_add(acc + 0, fx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(acc + 1, fy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(acc + 2, fz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cost) __hip_atomic_fetch_add(acc + 3, (unsigned long long)rays, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1441,7 +1460,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         sp = 0;                                                                                   \
         qn = 0;                                                                                   \
         if constexpr (WIDE) {   /* the root is slot 0 of a virtual node at base 0 */              \
-            inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                         \
+            if (PT_AB_CHEAP_START) inv = f3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)); \
+            else inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                    \
             const uint32_t oc_ = (inv.x < 0.0f ? 1u : 0u) | (inv.y < 0.0f ? 2u : 0u) | (inv.z < 0.0f ? 4u : 0u); \
             oct = oc_;                                                                            \
             tg = 0u;                                                                              \
@@ -1450,7 +1470,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             /* only camera rays can start far from the scene (a bounce starts on a primitive), and  \
                they all start at the camera: one uniform flag, set on the host (wideFar) */     \
             if (!INST && ((kargs()->camFar && depthLeft + 1 == kargs()->max_depth) ||              \
-                          (PT_WIDE_MIX && PT_MIX_CHECK && mixUnsafe(inv, kargs()->S.mixLim)))) {                  \
+                          (PT_WIDE_MIX && PT_MIX_CHECK && !PT_AB_CHEAP_START && mixUnsafe(inv, kargs()->S.mixLim)))) {                  \
                 ng = 0u;       /* origin far from the scene, or a direction the MIX planes */      \
                 oct |= 8u;     /* cannot take: the query in the reference's order (SHADE's redo) */ \
             }                                                                                     \

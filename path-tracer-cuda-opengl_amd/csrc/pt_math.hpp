@@ -88,3 +88,27 @@ __device__ __forceinline__ float min3Raw(float a, float b, float c) {
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// Sample mode: a block's fp32 sum as a 32.32 fixed-point integer (truncated toward zero; NaN -> 0,
+// saturated at +-2^62), and back (oracle/pt_oracle.cpp blockFixed / fixedToFloat, same roundings).
+// (Truncation done as two 32-bit halves of |p|: a * 2^-32 and a - hi * 2^32 are exact, hi has at
+// most 24 significant bits; fewer registers than the generic float -> int64 conversion.)
+__device__ __forceinline__ unsigned long long blockFixed(float x) {
+    const float p = x * 4294967296.0f;   // exact: a power-of-two scale
+    const float a = p == p ? fminf(fabsf(p), 0x1p62f) : 0.0f;
+    const uint32_t hi = (uint32_t)(a * 0x1p-32f);
+    const uint32_t lo = (uint32_t)__builtin_fmaf((float)hi, -0x1p32f, a);
+    const unsigned long long u = ((unsigned long long)hi << 32) | lo;
+    return p < 0.0f ? 0ull - u : u;
+}
+__device__ __forceinline__ float fixedToFloat(unsigned long long a) { return (float)((double)(long long)a * 0x1p-32); }
+// blockFixed for 0 <= x < 2^24 (every block sum of a scene whose radiance is bounded, e.g. by the
+// sky's <= 1 per sample): x = hi + frac with hi = trunc(x) (exact in float below 2^24) and frac = x -
+// hi exact, so trunc(x * 2^32) = hi * 2^32 + trunc(frac * 2^32) -- five VALU per channel instead of
+// the clamped, signed conversion's fourteen.  The same integer as blockFixed for such x (the
+// oracle's (int64_t)(x * 2^32)); -0 gives 0 either way.
+__device__ __forceinline__ unsigned long long blockFixedSmall(float x) {
+    const uint32_t hi = __float2uint_rz(x);
+    const float frac = x - (float)hi;
+    const uint32_t lo = __float2uint_rz(frac * 4294967296.0f);
+    return ((unsigned long long)hi << 32) | lo;
+}

@@ -30,6 +30,8 @@ def test_fast_reciprocal_equals_ieee_division_for_every_input():
     assert all(not (lo <= int(e) <= hi) for e in res["newton_mismatches_by_exponent"])
     # the draw mappings: uniformOf (one FMA) == x * 2^-32 + 2^-33, centered2Of == (u - 0.5f) * 2
     assert res["uniform_fma_mismatches"] == 0
+    # sample mode's fast fixed-point conversion of non-negative block sums below 2^24 (blockFixedSmall)
+    assert res["block_fixed_small_checked"] == 0x4B800000 + 1 and res["block_fixed_small_mismatches"] == 0
     assert res["centered2_fma_mismatches"] == 0
     assert out.returncode == 0
 

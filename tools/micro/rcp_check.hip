@@ -58,6 +58,23 @@ __global__ __launch_bounds__(256) void checkDraws(uint64_t base, unsigned long l
     if (mc) atomicAdd(&mis[1], mc);
 }
 
+// The sample-mode fixed-point conversions (pt_math.hpp): blockFixedSmall(x) == blockFixed(x) for
+// every fp32 x the kernels hand it (x >= 0 and x < 2^24, NaN excluded: all patterns 0 ... 0x4b7fffff
+// and -0), each of those patterns once.
+__global__ __launch_bounds__(256) void checkFixed(uint64_t base, unsigned long long* mis) {
+    unsigned long long m = 0ull, n = 0ull;
+    const uint64_t first = base + ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u;
+    for (int k = 0; k < 16; k++) {
+        const uint32_t bits = (uint32_t)(first + (uint64_t)k);
+        const float x = __uint_as_float(bits);
+        if (!(x >= 0.0f && x < 16777216.0f)) continue;
+        m += blockFixedSmall(x) != blockFixed(x) ? 1ull : 0ull;
+        n++;
+    }
+    if (m) atomicAdd(&mis[0], m);
+    if (n) atomicAdd(&mis[1], n);
+}
+
 int main() {
     unsigned long long *dExp = nullptr, *dRn = nullptr;
     if (hipMalloc(&dExp, 256 * sizeof(unsigned long long)) != hipSuccess ||
@@ -80,6 +97,15 @@ int main() {
     for (uint64_t base = 0; base < (1ull << 32); base += perLaunch) {
         hipLaunchKernelGGL(checkDraws, dim3((unsigned)(perLaunch / (256 * 16))), dim3(256), 0, 0, base, dDraw, 0x1p-32f, 2.0f);
     }
+    unsigned long long* dFix = nullptr;
+    if (hipMalloc(&dFix, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        fprintf(stderr, "hipMalloc failed\n");
+        return 2;
+    }
+    (void)hipMemset(dFix, 0, 2 * sizeof(unsigned long long));
+    for (uint64_t base = 0; base < (1ull << 32); base += perLaunch) {
+        hipLaunchKernelGGL(checkFixed, dim3((unsigned)(perLaunch / (256 * 16))), dim3(256), 0, 0, base, dFix);
+    }
     if (hipDeviceSynchronize() != hipSuccess) {
         fprintf(stderr, "kernel failed\n");
         return 2;
@@ -99,7 +125,10 @@ int main() {
     }
     unsigned long long hDraw[2] = {0ull, 0ull};
     (void)hipMemcpy(hDraw, dDraw, sizeof(hDraw), hipMemcpyDeviceToHost);
+    unsigned long long hFix[2] = {0ull, 0ull};
+    (void)hipMemcpy(hFix, dFix, sizeof(hFix), hipMemcpyDeviceToHost);
     printf("}, \"newton_mismatches_in_fast_range\": %llu, \"uniform_fma_mismatches\": %llu, "
-           "\"centered2_fma_mismatches\": %llu}\n", inRange, hDraw[0], hDraw[1]);
-    return (hRn == 0 && inRange == 0 && hDraw[0] == 0 && hDraw[1] == 0) ? 0 : 1;
+           "\"centered2_fma_mismatches\": %llu, \"block_fixed_small_checked\": %llu, \"block_fixed_small_mismatches\": %llu}\n",
+           inRange, hDraw[0], hDraw[1], hFix[1], hFix[0]);
+    return (hRn == 0 && inRange == 0 && hDraw[0] == 0 && hDraw[1] == 0 && hFix[0] == 0 && hFix[1] == 0x4b800000ull + 1ull) ? 0 : 1;
 }
