@@ -4677,10 +4677,13 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if (c) c->store(perCU, std::memory_order_relaxed);
         return PT_OK;
     };
-    // compat tile waves: the longest tiles of the launch order split into splitWays waves (renderKernelWF)
+    // compat tile waves: the longest tiles of the launch order split into splitWays waves (renderKernelWF).
+    // Only where a pixel's sequential chain can outlast the frame's throughput-bound part: long paths
+    // (max_depth > 16; C3, depth 50: 800 -> 766 ms).  Short-path frames are throughput-bound and the
+    // split's idle lanes cost (C5, depth 16: 548 -> 553 ms; C2, depth 8: +0.9 %).
     P.splitWays = std::max(1, std::min(8, envCount("PT_SPLIT_WAYS", 2)));
     P.splitTiles = (lpt && f->haveOrder && !sample && !cq && kernel != PT_KERNEL_SIMPLE)
-                       ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", 128))) : 0;
+                       ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", max_depth > 16 ? 128 : 0))) : 0;
     if (P.splitWays == 1) P.splitTiles = 0;
     P.compatGrid = P.ntiles + P.splitTiles * (P.splitWays - 1);
     if (cq) {
