@@ -175,6 +175,19 @@ def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
         return rc, log.read(), time.perf_counter() - t0
 
 
+def failure_digest(text, tail=2500):
+    """The lines of a multi-rank log that name a failure (a rank's FAILED line, timeouts, errors,
+    the watchdog's stack dumps and every rank's last traced phase) and then its tail."""
+    keys = ("FAILED", "Timeout", "Timed out", "Error", "error", "Traceback", "Thread 0x", "File \"")
+    picked = [ln for ln in text.splitlines() if any(k in ln for k in keys)]
+    phases = {}
+    for ln in text.splitlines():
+        if "] phase: " in ln:
+            phases[ln.split("]")[0] + "]"] = ln
+    return ("last phase per rank:\n" + "\n".join(phases.values()) + "\n--- failure lines:\n" +
+            "\n".join(picked[:80]) + "\n--- tail:\n" + text[-tail:])
+
+
 def last_json(text):
     import json
     return json.loads([x for x in text.splitlines() if x.startswith("{")][-1])

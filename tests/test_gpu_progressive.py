@@ -221,7 +221,7 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     assert rc == 0, log1[-3000:]
     rc, log2, _ = run_logged(_torchrun(2) + common[:1] + ["--gpus", "2"] + common[1:] + ["--png", two], 200, cwd=repo,
                              env=_rank_env(PT_DIST_BACKEND="gloo"), log_path=tmp_path / "r2.log")
-    assert rc == 0, log2[-3000:]
+    assert rc == 0, failure_digest(log2)
     np.testing.assert_array_equal(read_png(one), read_png(two))
     b = last_json(log2)
     assert [r["rank"] for r in b["per_rank"]] == [0, 1]
@@ -288,7 +288,7 @@ def test_bench_rccl_gather_one_rank(tmp_path, fif):
     assert (b.get("single_frame_ms") is not None) == (fif == 2)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(780)
 def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     """C4 (BASELINE.json configs[3]: the C3 scene at 1920x1080, 4096 spp, row-tiled over 8 GPUs)
     through bench.py's own multi-rank flow: 8 ranks over gloo sharing this one GPU (a rehearsal,
@@ -297,16 +297,19 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     byte and the rank-0 line reports the whole frame's rays and all eight ranks' figures."""
     import os
     import sys
-    from helpers import last_json, read_png, run_logged
+    from helpers import failure_digest, last_json, read_png, run_logged
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     common = ["bench.py", "--config", "c4", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-compat",
               "--no-interactive"]
     one, eight = str(tmp_path / "one.png"), str(tmp_path / "eight.png")
     rc, log1, _ = run_logged([sys.executable] + common + ["--png", one], 240, cwd=repo, log_path=tmp_path / "r1.log")
-    assert rc == 0, log1[-3000:]
-    rc, log8, _ = run_logged(_torchrun(8) + common[:1] + ["--gpus", "8"] + common[1:] + ["--png", eight], 300,
-                             cwd=repo, env=_rank_env(PT_DIST_BACKEND="gloo"), log_path=tmp_path / "r8.log")
-    assert rc == 0, log8[-3000:]
+    assert rc == 0, failure_digest(log1)
+    # eight processes share one GPU and the box's CPU share here: a rank can reach a collective
+    # minutes after another (start-up, serialised kernels), so the rehearsal's timeouts are wider
+    env = _rank_env(PT_DIST_BACKEND="gloo", PT_DIST_TIMEOUT="300", PT_BENCH_WATCHDOG="330")
+    rc, log8, wall = run_logged(_torchrun(8) + common[:1] + ["--gpus", "8"] + common[1:] + ["--png", eight], 480,
+                                cwd=repo, env=env, log_path=tmp_path / "r8.log")
+    assert rc == 0, f"8 ranks failed after {wall:.0f} s\n" + failure_digest(log8)
     np.testing.assert_array_equal(read_png(one), read_png(eight))
     l1, l8 = last_json(log1), last_json(log8)
     assert l1["config"]["spp"] == l8["config"]["spp"] == 4096 and l8["n_gpus"] == 8
