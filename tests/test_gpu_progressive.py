@@ -305,8 +305,10 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     rc, log1, _ = run_logged([sys.executable] + common + ["--png", one], 240, cwd=repo, log_path=tmp_path / "r1.log")
     assert rc == 0, failure_digest(log1)
     # eight processes share one GPU and the box's CPU share here: a rank can reach a collective
-    # minutes after another (start-up, serialised kernels), so the rehearsal's timeouts are wider
-    env = _rank_env(PT_DIST_BACKEND="gloo", PT_DIST_TIMEOUT="300", PT_BENCH_WATCHDOG="330")
+    # minutes after another (start-up, serialised kernels), so the rehearsal's timeouts are wider;
+    # the per-phase watchdog fires before the collective timeout, so a rank stuck in a phase dumps
+    # its own stack (faulthandler) before the others give up on it
+    env = _rank_env(PT_DIST_BACKEND="gloo", PT_DIST_TIMEOUT="300", PT_BENCH_WATCHDOG="240")
     rc, log8, wall = run_logged(_torchrun(8) + common[:1] + ["--gpus", "8"] + common[1:] + ["--png", eight], 480,
                                 cwd=repo, env=env, log_path=tmp_path / "r8.log")
     assert rc == 0, f"8 ranks failed after {wall:.0f} s\n" + failure_digest(log8)
