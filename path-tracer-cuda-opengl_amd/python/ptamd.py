@@ -95,6 +95,13 @@ EXPORTS = [
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} not built (run `make -C path-tracer-cuda-opengl_amd` or __graft_entry__.build())")
+# torch first when it is installed: libpt.so then binds the HIP runtime torch already loaded (one
+# runtime per process -- a second one, loaded after libpt.so's, sees no GPU: torch.cuda reports
+# "No HIP GPUs are available" although libpt.so works).  Torch stays optional for the C ABI.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
 lib = C.CDLL(LIB_PATH)
 
 _P = C.c_void_p

@@ -23,12 +23,13 @@ import datetime
 import faulthandler
 import os
 import sys
+import time
 import traceback
 from contextlib import contextmanager
 
 import numpy as np
 
-_STATE = {"rank": 0, "world": 1, "phase": "start", "watchdog_s": 0.0, "backend": None}
+_STATE = {"rank": 0, "world": 1, "phase": "start", "watchdog_s": 0.0, "backend": None, "t0": time.monotonic()}
 
 
 def init(backend: str, rank: int, world: int, device=None, timeout_s: float = 120.0, watchdog_s: float = 0.0) -> None:
@@ -53,7 +54,7 @@ def phase(name: str) -> None:
     re-arm the watchdog for it."""
     _STATE["phase"] = name
     if os.environ.get("PT_DIST_TRACE") == "1":
-        sys.stderr.write(f"{tag()} phase: {name}\n")
+        sys.stderr.write(f"{tag()} phase: {name} (t = {time.monotonic() - _STATE['t0']:.1f} s)\n")
         sys.stderr.flush()
     if _STATE["watchdog_s"] > 0:
         sys.stderr.flush()
