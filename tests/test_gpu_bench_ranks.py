@@ -1,0 +1,155 @@
+"""GPU tests: bench.py's multi-rank flow run as separate processes: row stripes
+over ranks, the gather to rank 0 and the un-permuted PNG equal to the 1-rank PNG (gloo ranks sharing
+the box's one GPU, and RCCL with the one rank a one-GPU box allows), the fail-fast of a failing
+rank, and the C4 8-rank rehearsal.
+
+These tests start their own GPU processes (up to 8 ranks).  They live in a file of their own that
+sorts first among the GPU tests, so they run before the suite's own process has created any GPU
+state: after ~300 in-process tests the same 8-rank rehearsal took 171 s instead of 39 s with the
+suite process's GPU context alive beside its ranks (not pinned down further; the rehearsal's
+timeouts leave room for either).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def free_port() -> str:
+    """A free TCP port on 127.0.0.1 for a torch.distributed.run rendezvous (a fixed port can still be
+    held by an earlier run on a shared box)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return str(sk.getsockname()[1])
+
+
+def _torchrun(n, port=None):
+    import sys
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", port or free_port()]
+
+
+def _rank_env(**kw):
+    """Multi-rank runs of bench.py: phases traced to stderr (PT_DIST_TRACE), gloo bound to the
+    loopback interface (the rendezvous is 127.0.0.1; gloo would otherwise pick the interface the
+    host name resolves to), a collective timeout and a watchdog well below the subprocess timeout."""
+    import os
+    env = dict(os.environ, PT_DIST_TRACE="1", GLOO_SOCKET_IFNAME="lo", PT_DIST_TIMEOUT="60", PT_BENCH_WATCHDOG="150")
+    env.update(kw)
+    return env
+
+
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
+    """bench.py's multi-rank flow (stripe partition, per-rank RGBA8 frames, gather, un-permute,
+    PNG) rehearsed with two ranks sharing the GPU over gloo: the PNG equals the 1-rank PNG, and the
+    N > 1 line carries the per-rank kernel / gather figures and one frame's latency beside the
+    pipelined (two frames in flight) rate."""
+    import os
+    import sys
+    from helpers import last_json, read_png, run_logged
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--config", "c2", "--spp", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+              "--no-compat"]
+    one, two = str(tmp_path / "one.png"), str(tmp_path / "two.png")
+    rc, log1, _ = run_logged([sys.executable] + common + ["--png", one], 150, cwd=repo, log_path=tmp_path / "r1.log")
+    assert rc == 0, log1[-3000:]
+    rc, log2, _ = run_logged(_torchrun(2) + common[:1] + ["--gpus", "2"] + common[1:] + ["--png", two], 200, cwd=repo,
+                             env=_rank_env(PT_DIST_BACKEND="gloo"), log_path=tmp_path / "r2.log")
+    assert rc == 0, failure_digest(log2)
+    np.testing.assert_array_equal(read_png(one), read_png(two))
+    b = last_json(log2)
+    assert [r["rank"] for r in b["per_rank"]] == [0, 1]
+    assert all(r["kernel_ms"] > 0 and r["gather_ms"] >= 0 and r["rays_per_frame"] > 0 for r in b["per_rank"])
+    assert sum(r["rays_per_frame"] for r in b["per_rank"]) == b["config"]["rays_per_frame"]
+    assert b["config"]["frames_in_flight"] == 2 and b["single_frame_ms"] > 0
+    assert "[rank 1/2] phase: timed frames" in log2
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("kind", ["raise", "mismatch", "hang"])
+def test_bench_failing_rank_ends_every_rank(tmp_path, kind):
+    """Fail-fast of bench.py's multi-rank flow (two gloo ranks sharing the GPU): rank 1 fails just
+    before the timed frames (PT_BENCH_INJECT: an exception, a frame that differs from the
+    reference-order frame, or a hang) and BOTH ranks exit non-zero, well within the collective
+    timeout + watchdog, with the failure named by rank and phase."""
+    import os
+    import sys
+    from helpers import run_logged
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    where = "timed frames" if kind == "mismatch" else "timed"
+    cmd = _torchrun(2) + ["bench.py", "--gpus", "2", "--config", "c2", "--spp", "4", "--steps", "2", "--warmup", "1",
+                          "--no-cpu-baseline", "--no-compat"]
+    env = _rank_env(PT_DIST_BACKEND="gloo", PT_BENCH_INJECT=f"1:{where}:{kind}", PT_DIST_TIMEOUT="20",
+                    PT_BENCH_WATCHDOG="40", TORCHELASTIC_ERROR_FILE=str(tmp_path / "err.json"))
+    rc, log, wall = run_logged(cmd, 240, cwd=repo, env=env, log_path=tmp_path / "fail.log")
+    assert rc != 0, log[-3000:]
+    if kind == "raise":
+        assert "[rank 1/2] FAILED in phase 'timed frames'" in log and "injected failure" in log, log[-3000:]
+    elif kind == "mismatch":   # every rank learns of it (agree) and exits with it
+        assert log.count("frame differs from the reference-order frame on rank(s) [1]") == 2, log[-3000:]
+    else:   # the peer's collective times out (20 s) or the hung rank's watchdog (40 s) fires first
+        assert "Timed out" in log or "Timeout (0:00:40)" in log or "FAILED" in log, log[-3000:]
+    assert wall < 200, wall
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("fif", [1, 2])
+def test_bench_rccl_gather_one_rank(tmp_path, fif):
+    """bench.py's multi-rank flow over RCCL (backend "nccl": process group, dist.gather of the
+    RGBA8 stripes, barriers, max / sum reductions) with the one rank a one-GPU box allows
+    (PT_DIST_FORCE=1): the PNG equals the plain 1-rank PNG and the reported rays are the frame's.
+    fif 2: frames in flight as N > 1 runs them (two films on two streams, each frame's gather
+    enqueued on its own stream, three timed frames so both films alternate)."""
+    import os
+    import sys
+    from helpers import last_json, read_png, run_logged
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--config", "c2", "--spp", "4", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+              "--no-compat", "--no-interactive"]
+    one, forced = str(tmp_path / "one.png"), str(tmp_path / "rccl.png")
+    rc, log1, _ = run_logged([sys.executable] + common + ["--png", one], 150, cwd=repo, log_path=tmp_path / "r1.log")
+    assert rc == 0, log1[-3000:]
+    rc, log2, _ = run_logged(_torchrun(1) + common[:1] + ["--gpus", "1"] + common[1:] +
+                             ["--png", forced, "--frames-in-flight", str(fif), "--steps", "3"], 200, cwd=repo,
+                             env=_rank_env(PT_DIST_FORCE="1", PT_DIST_BACKEND="nccl"), log_path=tmp_path / "r2.log")
+    assert rc == 0, log2[-3000:]
+    np.testing.assert_array_equal(read_png(one), read_png(forced))
+    a, b = last_json(log1), last_json(log2)
+    assert a["config"]["rays_per_frame"] == b["config"]["rays_per_frame"] > 0
+    assert b["config"]["frames_in_flight"] == fif and b["steps"] == 3
+    # the RCCL gather's own time, from HIP events on the frame's stream
+    assert len(b["per_rank"]) == 1 and b["per_rank"][0]["gather_ms"] > 0
+    assert (b.get("single_frame_ms") is not None) == (fif == 2)
+
+
+@pytest.mark.timeout(780)
+def test_bench_c4_eight_ranks_rehearsal(tmp_path):
+    """C4 (BASELINE.json configs[3]: the C3 scene at 1920x1080, 4096 spp, row-tiled over 8 GPUs)
+    through bench.py's own multi-rank flow: 8 ranks over gloo sharing this one GPU (a rehearsal,
+    never a reported number), each rendering its 1/8 of the stripes at the full sample count on the
+    wide tree its own device built; the gathered, un-permuted PNG equals the 1-rank PNG byte for
+    byte and the rank-0 line reports the whole frame's rays and all eight ranks' figures."""
+    import os
+    import sys
+    from helpers import failure_digest, last_json, read_png, run_logged
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--config", "c4", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-compat",
+              "--no-interactive"]
+    one, eight = str(tmp_path / "one.png"), str(tmp_path / "eight.png")
+    rc, log1, _ = run_logged([sys.executable] + common + ["--png", one], 240, cwd=repo, log_path=tmp_path / "r1.log")
+    assert rc == 0, failure_digest(log1)
+    # eight processes share one GPU and the box's CPU share here: a rank can reach a collective
+    # minutes after another (start-up, serialised kernels), so the rehearsal's timeouts are wider;
+    # the per-phase watchdog fires before the collective timeout, so a rank stuck in a phase dumps
+    # its own stack (faulthandler) before the others give up on it
+    env = _rank_env(PT_DIST_BACKEND="gloo", PT_DIST_TIMEOUT="300", PT_BENCH_WATCHDOG="240")
+    rc, log8, wall = run_logged(_torchrun(8) + common[:1] + ["--gpus", "8"] + common[1:] + ["--png", eight], 480,
+                                cwd=repo, env=env, log_path=tmp_path / "r8.log")
+    assert rc == 0, f"8 ranks failed after {wall:.0f} s\n" + failure_digest(log8)
+    np.testing.assert_array_equal(read_png(one), read_png(eight))
+    l1, l8 = last_json(log1), last_json(log8)
+    assert l1["config"]["spp"] == l8["config"]["spp"] == 4096 and l8["n_gpus"] == 8
+    assert l1["config"]["rays_per_frame"] == l8["config"]["rays_per_frame"] > 4 * 1920 * 1080 * 4096
+    assert len(l8["per_rank"]) == 8 and "lbvh_plus_wide_tree_device_ms" in l8["scene_build"]
