@@ -620,7 +620,10 @@ __device__ __forceinline__ bool wideFar(const DevScene& S, float3 o) { return wi
 // Instanced scenes draw the line at 2 world extents: their mesh trees are quantised for origins
 // within that reach (buildInstanced), 4x finer planes than 8 extents would allow (c5i 503 -> 498
 // ms); farther origins start at their entry into the world (instEntry).
-constexpr float kInstFarExt = 2.0f;
+#ifndef PT_INST_FAR_EXT
+#define PT_INST_FAR_EXT 2.0f
+#endif
+constexpr float kInstFarExt = PT_INST_FAR_EXT;
 static_assert(kInstFarExt >= 1.0f, "instEntry's cube (centre +- ext) must lie inside the quantised reach");
 __device__ __forceinline__ bool instFar(const DevScene& S, float3 o) {
     const float m = fmaxf(fmaxf(fabsf(o.x - S.cx), fabsf(o.y - S.cy)), fabsf(o.z - S.cz));

@@ -153,3 +153,21 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     assert l1["config"]["spp"] == l8["config"]["spp"] == 4096 and l8["n_gpus"] == 8
     assert l1["config"]["rays_per_frame"] == l8["config"]["rays_per_frame"] > 4 * 1920 * 1080 * 4096
     assert len(l8["per_rank"]) == 8 and "lbvh_plus_wide_tree_device_ms" in l8["scene_build"]
+
+
+@pytest.mark.timeout(200)
+def test_binding_before_torch_shares_one_hip_runtime(tmp_path):
+    """A process that imports the binding before torch: torch must still see the GPU (the binding
+    loads torch first, so libpt.so binds torch's HIP runtime instead of a second one), and a
+    device tensor and a libpt call work side by side.  Its own process: the suite's has torch."""
+    import os
+    import sys
+    from helpers import run_logged
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, 'path-tracer-cuda-opengl_amd/python'); import ptamd; import torch; "
+            "x = torch.ones(64, device='cuda:0'); n = ptamd.device_count(); "
+            "print('ok', float(x.sum()), n, torch.cuda.device_count())")
+    rc, log, _ = run_logged([sys.executable, "-c", code], 150, cwd=repo, log_path=tmp_path / "bind.log")
+    assert rc == 0, log[-3000:]
+    line = [ln for ln in log.splitlines() if ln.startswith("ok ")][-1].split()
+    assert float(line[1]) == 64.0 and int(line[2]) > 0 and int(line[3]) > 0, line
