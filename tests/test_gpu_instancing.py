@@ -309,3 +309,34 @@ def test_far_camera_instanced_render(pt, gpu):
     rd, std = pt.render(si, pt.Film(w, h, 3, device=gpu), cam, spp, ip.max_depth, kernel=pt.KERNEL_WIDE,
                         rng=pt.RNG_SAMPLE)
     assert np.isfinite(rd).all() and std.paths == w * h * spp
+
+
+@pytest.mark.parametrize("rng", ["sample", "compat"])
+def test_instanced_frame_independent_of_scheduling(pt, gpu, rng):
+    """The instanced kernels' frame is a function of scene, camera, seed and spp only, as the
+    flattened kernels' is (pt.h: neither the scheduling nor the stripe partition changes the image):
+    other LEAF / SHADE thresholds (the instanced defaults are 16 / 20), the identity launch order and
+    a 2-way partition of 8-row stripes give the same bits and rays."""
+    w, h, spp = 96, 54, 4
+    ip = pt.InstancedPreset("bunny_field", w, h)
+    s = instanced_scene(pt, ip, gpu)
+    r = pt.RNG_SAMPLE if rng == "sample" else pt.RNG_COMPAT
+
+    def frame(film_kw=None, **kw):
+        f = pt.Film(w, h, 7, device=gpu, **(film_kw or {}))
+        img, st = pt.render(s, f, ip.camera, spp, ip.max_depth, kernel=pt.KERNEL_WIDE, rng=r, **kw)
+        return img, st, f
+
+    a, sa, _ = frame()
+    for kw in ({"leaf_batch": 5, "shade_batch": 40}, {"leaf_batch": 40, "shade_batch": 6},
+               {"flags": pt.IDENTITY_ORDER}):
+        b, sb, _ = frame(**kw)
+        np.testing.assert_array_equal(b.view(np.uint32), a.view(np.uint32), err_msg=str(kw))
+        assert sb.rays == sa.rays, kw
+    full = a.reshape(h, w, 3)
+    rays = 0
+    for part in (0, 1):
+        img, st, f = frame({"stripe_height": 8, "n_parts": 2, "part": part})
+        np.testing.assert_array_equal(img.reshape(-1, w, 3).view(np.uint32), full[f.rows].view(np.uint32))
+        rays += st.rays
+    assert rays == sa.rays
