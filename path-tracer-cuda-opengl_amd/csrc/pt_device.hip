@@ -270,7 +270,11 @@ __device__ __forceinline__ uint32_t shlOpaque(uint32_t x) {
     asm("v_lshlrev_b32 %0, %1, %2" : "=v"(t) : "i"(S), "v"(x));
     return t;
 }
-__device__ __forceinline__ uint32_t mul80(uint32_t x) { return shlOpaque<6>(x) + (x << 4); }   // x < 2^26
+// byte offset of node slot x (80-B slots: x < 2^26; 128-B slots, PT_NODE_DWORDS 32: x < 2^25)
+__device__ __forceinline__ uint32_t mul80(uint32_t x) {
+    if constexpr (pt::kW8NodeDwords == 32) return x << 7;
+    return shlOpaque<6>(x) + (x << 4);
+}
 __device__ __forceinline__ uint32_t mul48(uint32_t x) { return shlOpaque<5>(x) + (x << 4); }   // x < 2^27
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));

@@ -22,6 +22,7 @@
 #include <cstring>
 
 #include "pt_prims.hpp"
+#include "pt_wide8.hpp"
 #include "pt_wide_dev.hpp"
 
 namespace pt {
@@ -512,7 +513,7 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
     R[5] = myPrims;
     R[6] = meta[0];
     R[7] = meta[1];
-    uint4* dst = reinterpret_cast<uint4*>(nodes + 20 * (size_t)item.y);
+    uint4* dst = reinterpret_cast<uint4*>(nodes + (size_t)pt::kW8NodeDwords * (size_t)item.y);
     for (int q = 0; q < 5; q++) dst[q] = make_uint4(R[4 * q], R[4 * q + 1], R[4 * q + 2], R[4 * q + 3]);
 }
 

@@ -12,7 +12,11 @@
 
 namespace pt {
 
-constexpr int kW8NodeDwords = 20;   // 80-B node record (layout in pt_wide8.cpp)
+#ifndef PT_NODE_DWORDS
+#define PT_NODE_DWORDS 20   // a node slot: the 80-B record; 32 pads each slot to one 128-B cache line (A/B builds)
+#endif
+constexpr int kW8NodeDwords = PT_NODE_DWORDS;   // node slot in dwords: 80-B record (layout in pt_wide8.cpp) + padding
+static_assert(kW8NodeDwords == 20 || kW8NodeDwords == 32, "node slots of 80 or 128 B");
 constexpr int kW8PrimDwords = 12;   // 48-B primitive record
 
 struct Wide8 {

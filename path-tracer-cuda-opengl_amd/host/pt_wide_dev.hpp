@@ -29,7 +29,7 @@ struct WideDevIn {
 };
 
 struct WideDevOut {
-    uint32_t* nodes;           // node slots x 20 dwords, capacity wideDevNodeSlots(n)
+    uint32_t* nodes;           // node slots x kW8NodeDwords dwords, capacity wideDevNodeSlots(n)
     uint32_t* wprims;          // n x 12 dwords
     float4* wshade;            // n x 3 float4, shading records in reference rank order
     uint32_t* rank;            // n: leaf k -> its rank in the reference's traversal order
