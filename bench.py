@@ -30,10 +30,12 @@ instructions) come from the committed profiles of the SAME libpt.so build (`buil
 else null.  `cpu_baseline` = the CPU restatement (oracle/) on the host cores, rank 0 at N = 1 only,
 on a bounded sample.  `interactive` (N = 1) = frames/s of the progressive interactive mode at
 1 / 4 / 16 spp.  Every timed frame is compared with the reference-order kernel's frame (pixels
-and rays).  With N > 1 consecutive steps alternate between two films on two streams (two frames
-in flight: a frame's first waves overlap the previous frame's tail, which is 7 % of a 1/8 share);
-`ms_per_step` is then the wall time per frame of the sequence, and the roofline's launch duration
-is taken from a warmup launch that ran alone.
+and rays).  The headline renders one frame at a time at every N, with the host-built wide tree
+at every N (the same method for N = 1 and N = 8: the driver divides their ms_per_step).  The
+`pipelined` figure beside it repeats the timed sequence with two frames in flight: consecutive
+steps alternate between two films on two streams, so a frame's first waves overlap the previous
+frame's tail (7 % of a 1/8 share).  (--frames-in-flight 2 makes that the headline; its roofline
+launch duration is then taken from a warmup launch that ran alone.)
 """
 import argparse
 import json
@@ -59,6 +61,8 @@ CONFIGS = {
     "c2": ("cornell", "Cornell box (32 tris) 800x800 @256spp depth 8 (C2)"),
     "c5": ("bunny_field", "1,043,312-tri bunny field 1920x1080 @512spp depth 16 (C5)"),
     "c4": ("bunny_cornell", "bunny-in-Cornell (5,000 tris) 1920x1080 @4096spp depth 50 (C4, the 8-GPU config)"),
+    "c5x4": ("bunny_field_x4", "C5 at 4x the triangles: 840 half-size bunnies, 4,173,152 tris 1920x1080 @128spp "
+                               "depth 16 (a flattened tree beyond the 256 MB Infinity Cache; not a BASELINE config)"),
     "c5i": ("bunny_field", "bunny field instanced: 5,000 tris stored once, 211 instances (1,043,312 tris placed) "
                            "1920x1080 @512spp depth 16 (C5, two-level tree)"),
 }
@@ -227,7 +231,7 @@ def interactive(scene, preset, dev, stream, local, frames=(30, 20, 10), spps=(1,
     return out
 
 
-def main() -> None:
+def make_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
@@ -251,11 +255,17 @@ def main() -> None:
                          "PngImage::saveColor, 4 B/pixel on the wire) or f32 (linear-sqrt RGB, 12 B/pixel)")
     ap.add_argument("--png", default="", help="rank 0 writes the last (assembled) frame to this PNG")
     ap.add_argument("--frames-in-flight", type=int, default=0, choices=[0, 1, 2],
-                    help="frames rendered concurrently on two streams (0 = 2 for N > 1, 1 for N = 1)")
+                    help="frames rendered concurrently on two streams for the headline (0 = 1 at every N)")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the `pipelined` figure (the timed sequence again with two frames in flight)")
     ap.add_argument("--kernel", default="wide", choices=["wide", "wavefront"],
                     help="wide (default): the compressed 8-wide SAH tree, nearest child first; wavefront: the "
                          "binary LBVH in the reference's visiting order.  Same image either way")
-    args = ap.parse_args()
+    return ap
+
+
+def main() -> None:
+    args = make_parser().parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -301,8 +311,17 @@ def injected(rank: int, where: str) -> str:
     return kind
 
 
+def run_settings(args, world: int) -> dict:
+    """The method of a run, identical at every N unless a flag or knob says otherwise (the driver
+    divides the N = 1 and N = 8 lines' ms_per_step; both must measure the same thing): one frame at
+    a time, the wide tree from the host SAH build.  tests/test_host.py checks it for N = 1, 2, 8."""
+    return {"frames_in_flight": args.frames_in_flight or 1,
+            "wide_tree": "device" if os.environ.get("PT_BENCH_WIDE_DEVICE", "0") == "1" else "host"}
+
+
 def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: bool) -> None:
     phase = ptdist.phase
+    settings = run_settings(args, world)
 
     if world > 1 and "PT_BUILD_THREADS" not in os.environ:
         # the ranks of a node share its host cores: each rank's host wide-tree build (before the
@@ -323,20 +342,24 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
         scene.build_bvh()
         scene_build = {"two_level_tree_host_ms": scene.build_ms, "device_bytes": scene.bvh_info()["device_bytes"]}
     else:
-        # N > 1: every rank builds the wide tree on its own GPU (PT_BVH_WIDE_DEVICE: top-down SAH, the
-        # host build's quality, C5 7 ms) instead of 8 ranks sharing the node's host cores for the host
-        # SAH build (C5 0.75 s on 16 threads); the frames are the same (closest hits do not depend on
-        # the tree).  PT_BENCH_WIDE_DEVICE=0/1 overrides.
-        wide_dev = os.environ.get("PT_BENCH_WIDE_DEVICE", "1" if world > 1 else "0") == "1"
+        # The same tree builder at every N (the driver's 1 -> 8 ratio compares one method): the host
+        # SAH build (before the timed frames; with N > 1 each rank takes its share of the host cores,
+        # PT_BUILD_THREADS).  PT_BENCH_WIDE_DEVICE=1 builds it on each rank's device instead (top-down
+        # SAH of the host build's quality, C5 7 ms); the frames are the same either way (closest hits
+        # do not depend on the tree).
+        wide_dev = settings["wide_tree"] == "device"
         flags = ptamd.PT_BVH_ORIGIN_BOUNDS | (ptamd.PT_BVH_WIDE_DEVICE if wide_dev else 0)
         scene = ptamd.Scene(preset.objects, preset.materials, device=local, flags=flags)
         scene.build_bvh(flags)   # again: the first build in a process also pays one-time module loading
         scene_build = {"lbvh_device_ms" if not wide_dev else "lbvh_plus_wide_tree_device_ms": scene.build_ms}
-    # Frames in flight (N > 1; --frames-in-flight): consecutive steps alternate between two films
-    # (and output buffers) on two streams, so a frame's first waves start while the previous
-    # frame's last paths finish -- the launch's tail, 7 % of a 1/8 share of C3 but 0.2 % of the
-    # whole frame (tools/pipe_frames.py), so N = 1 renders one frame at a time.  Every frame is
-    # still rendered in full and checked against the reference-order frame.
+    # Frames in flight (--frames-in-flight, default 1 at every N): with 2, consecutive steps
+    # alternate between two films (and output buffers) on two streams, so a frame's first waves
+    # start while the previous frame's last paths finish -- the launch's tail, 7 % of a 1/8 share of
+    # C3 but 0.2 % of the whole frame (tools/pipe_frames.py).  The headline renders one frame at a
+    # time at every N (one method for the driver's ratio; the render kernel's launches run alone, so
+    # their HIP-event and rocprof durations are the frame's); the `pipelined` figure beside it is the
+    # same sequence with two frames in flight.  Every frame is still rendered in full and checked
+    # against the reference-order frame.
     films = [ptamd.Film(w, h, args.seed, device=local, stripe_height=STRIPE, n_parts=world, part=rank) for _ in range(2)]
     max_rows = ptdist.max_rows(h, STRIPE, world)
     rgba8 = args.output == "rgba8"
@@ -376,9 +399,10 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
                     if ev:
                         ev[1].record(s)
                         gather_ev.append(ev)
-                else:
+                else:   # (gloo: host staging; the gather's own time, not the render it waits for)
+                    host = buf.cpu()
                     tg0 = time.perf_counter()
-                    g = ptdist.gather_to_root(buf.cpu(), world, rank)
+                    g = ptdist.gather_to_root(host, world, rank)
                     if rank == 0:
                         gathered[j].copy_(g)
                     if timed:
@@ -420,7 +444,7 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
         return st
 
     check(ref_st, 0, "reference-order frame")   # (also loads torch's comparison kernels before the timed region)
-    fif = args.frames_in_flight or (2 if world > 1 else 1)
+    fif = settings["frames_in_flight"]
     warm_kms = ref_st.kernel_ms
     phase("warmup frames")
     if fif == 2:
@@ -512,6 +536,42 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
             dist.all_reduce(sf, op=dist.ReduceOp.MAX)
         single_frame_ms = float(sf.item())
         agree("single frame")
+    pipelined = None
+    if args.steps > 0 and fif == 1 and not args.no_pipelined:
+        # The same timed sequence with two frames in flight (films 0 / 1 on two streams, each frame
+        # still rendered in full, gathered and checked): the launches' tails overlap the next frame's
+        # first waves.  Reported beside the one-frame-at-a-time headline, never instead of it.
+        phase("pipelined frames")
+        check(frame(1, wait=True), 1, "pipelined frames")   # film 1's first launch: its tile order
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter()
+        prays, infl = 0, []
+        for k in range(args.steps):
+            if len(infl) == 2:
+                prays += finish(infl.pop(0), "pipelined frames").rays
+            frame(k % 2)
+            infl.append(k % 2)
+        for j in infl:
+            prays += finish(j, "pipelined frames").rays
+        torch.cuda.synchronize(dev)
+        if dist_on:
+            dist.barrier()
+        pt_ = torch.tensor([time.perf_counter() - tp, float(prays)], dtype=torch.float64, device=tdev)
+        if dist_on:
+            pmx, psm = pt_[:1].clone(), pt_[1:].clone()
+            dist.all_reduce(pmx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(psm, op=dist.ReduceOp.SUM)
+            pel, ptot = float(pmx.item()), float(psm.item())
+        else:
+            pel, ptot = float(pt_[0].item()), float(pt_[1].item())
+        agree("pipelined frames")
+        pipelined = {"frames_in_flight": 2, "steps": args.steps, "ms_per_step": pel / args.steps * 1e3,
+                     "value": ptot / pel / 1e6, "unit": "Mray/s",
+                     "note": "the timed sequence again with two frames in flight (two films on two streams: a "
+                             "frame's first waves overlap the previous frame's tail), max over ranks; the headline "
+                             "renders one frame at a time at every N"}
     phase("report")
 
     compat = None
@@ -572,6 +632,7 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
             "data": "synthetic: scene assembled from the reference's bundled OBJ models (models/), fixed seed",
             "config": {"workload": workload, "width": w, "height": h, "spp": spp, "max_depth": depth,
                        "stripe_rows": STRIPE, "parallelism": f"rows{world}", "frames_in_flight": fif,
+                       "wide_tree": settings["wide_tree"] if not instanced else "host two-level",
                        "output": ("rgba8: quantised on the device like PngImage::saveColor, gathered at 4 B/pixel"
                                   if rgba8 else "f32 RGB, gathered at 12 B/pixel"),
                        "rays_per_frame": total_rays / args.steps,
@@ -620,6 +681,8 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
             out["single_frame_note"] = ("one frame rendered alone after the timed frames (no frame in flight beside "
                                         "it), max over ranks; ms_per_step is the pipelined rate with "
                                         f"frames_in_flight {fif}")
+        if pipelined is not None:
+            out["pipelined"] = pipelined
         if compat:
             out["compat_mode"] = compat
         if world == 1 and not args.no_interactive:

@@ -108,7 +108,8 @@ int pt_camera_make(const float from[3], const float at[3], float vfov_deg, float
 int pt_camera_move(pt_camera* cam, int dir, float delta_time);
 /* Scene builders.  name: "triangle_world" (main.cu:119-196, the reference default),
  * "random_world" (main.cu:198-256), "test_world" (main.cu:57-117), "rtiow" (C1),
- * "cornell" (C2), "bunny_cornell" (C3), "bunny_field" (C5).  models_dir holds
+ * "cornell" (C2), "bunny_cornell" (C3), "bunny_field" (C5), "bunny_field_x4" (C5 at 4x the
+ * triangles: 840 half-size bunnies, an HBM-resident stress case).  models_dir holds
  * cornellbox/<part>.obj and bunny/bunny.obj.  width/height <= 0 keep the preset's frame. */
 int pt_preset_scene(const char* name, const char* models_dir, int width, int height, pt_scene_desc* out);
 void pt_scene_desc_free(pt_scene_desc* desc);

@@ -48,6 +48,7 @@ for name, res, args in [
     ("orc_xorwow_skip_subsequences", None, [_P, C.c_uint64]),
     ("orc_xorwow_next", C.c_uint32, [_P]),
     ("orc_curand_uniform", C.c_float, [_P]),
+    ("orc_set_draw_order", None, [C.c_int]),
     ("orc_morton_keys", C.c_int, [_P, C.c_int64, C.c_int, _P]),
     ("orc_build_lbvh", C.c_int, [_P, C.c_int64, _P, C.c_int, _P]),
     ("orc_bvh_depth", C.c_int, [_P, C.c_int64]),
@@ -108,6 +109,13 @@ def curand_uniform(state: np.ndarray, count: int) -> np.ndarray:
     """Draw `count` uniforms; `state` (uint32[6]) is advanced in place."""
     assert state.dtype == np.uint32 and state.flags["C_CONTIGUOUS"]
     return np.array([lib.orc_curand_uniform(state.ctypes.data) for _ in range(count)], np.float32)
+
+
+def set_draw_order(zyx: bool) -> None:
+    """Test-only: draw vec3(u - 0.5f, u - 0.5f, u - 0.5f)'s three coordinates z, y, x instead of x, y, z.
+    utility.h:55-58 / 76-79 leave the order to the compiler (C++ argument evaluation order is
+    unspecified); the oracle's default x, y, z is an assumption (pt_oracle.cpp draw3)."""
+    lib.orc_set_draw_order(1 if zyx else 0)
 
 
 def morton_keys(objects: np.ndarray, include_origin: bool = True) -> np.ndarray:

@@ -315,14 +315,24 @@ struct TapeRng {
 };
 
 // ------------------------------------------------------------ samplers (utils/utility.h)
-// vec3(curand_uniform()-0.5f, ...) arguments are drawn x, y, z in that order.
+// ASSUMPTION (parity unpinned): utility.h:55-58 and :76-79 build the candidate as
+// vec3(curand_uniform(s) - 0.5f, curand_uniform(s) - 0.5f, curand_uniform(s) - 0.5f).  C++ leaves
+// the evaluation order of constructor arguments unspecified, so which coordinate gets the first
+// draw is whatever nvcc emitted; no reference binary or output pins it.  The oracle (and the HIP
+// kernels) draw x, y, z in that order (clang's left-to-right order).  orc_set_draw_order(1) draws
+// z, y, x instead (g++'s / MSVC's right-to-left order for host code) -- test-only, to show what the
+// statistical pins can and cannot see (tests/test_oracle.py::test_draw_order_is_unpinned_by_block_means).
+static int g_drawZYX = 0;
+template <class R> inline void draw3(R& rng, float& a, float& b, float& c) {
+    if (g_drawZYX) { c = rng() - 0.5f; b = rng() - 0.5f; a = rng() - 0.5f; }
+    else { a = rng() - 0.5f; b = rng() - 0.5f; c = rng() - 0.5f; }
+}
 template <class R> V3 randomOnUnitSphereDiscard(R& rng) {                              // :51-62
     V3 res;
     float norm;
     do {
-        float a = rng() - 0.5f;
-        float b = rng() - 0.5f;
-        float c = rng() - 0.5f;
+        float a, b, c;
+        draw3(rng, a, b, c);
         res = 2.0f * v3(a, b, c);
         norm = len2(res);
     } while (len2(res) >= 1.0f);
@@ -331,9 +341,8 @@ template <class R> V3 randomOnUnitSphereDiscard(R& rng) {                       
 template <class R> V3 randomInUnitSphereDiscard(R& rng) {                              // :73-82
     V3 res;
     do {
-        float a = rng() - 0.5f;
-        float b = rng() - 0.5f;
-        float c = rng() - 0.5f;
+        float a, b, c;
+        draw3(rng, a, b, c);
         res = 2.0f * v3(a, b, c);
     } while (len2(res) >= 1.0f);
     return res;
@@ -513,6 +522,7 @@ void orc_xorwow_init_range(uint64_t seed, uint64_t first, int64_t count, uint32_
 }
 
 uint32_t orc_xorwow_next(uint32_t s[6]) { return xorwowNext(s); }
+void orc_set_draw_order(int zyx) { g_drawZYX = zyx ? 1 : 0; }   // test-only: see draw3
 float orc_curand_uniform(uint32_t s[6]) { return curandUniform(s); }
 
 int orc_morton_keys(const orc_object* objs, int64_t n, int include_origin, uint64_t* keys) {

@@ -47,6 +47,8 @@ void orc_xorwow_init_range(uint64_t seed, uint64_t first, int64_t count, uint32_
 void orc_xorwow_skip_subsequences(uint32_t state[6], uint64_t n);   /* state := state after n*2^67 draws */
 uint32_t orc_xorwow_next(uint32_t state[6]);
 float orc_curand_uniform(uint32_t state[6]);
+/* test-only: 1 = the three draws of vec3(u-0.5f, u-0.5f, u-0.5f) taken z, y, x (an unpinned choice, see draw3) */
+void orc_set_draw_order(int zyx);
 
 /* utils/morton_code.h:29-75; include_origin=1 reproduces maxBox starting as the zero box */
 int orc_morton_keys(const orc_object* objs, int64_t n, int include_origin, uint64_t* keys_out);

@@ -988,7 +988,8 @@ struct RenderParams {
     const uint32_t* tileXY;                   // sample mode: tile of each launch slot as tx | ty << 16 (the order decoded)
     int nblocksShift;                         // sample mode: log2(ngroups) when a power of two, else -1
     unsigned* tileCost;                       // out: per-tile wave duration (s_memrealtime ticks, 100 MHz)
-    int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio 2
+    int prioTiles;                            // the first prioTiles tiles of the order run at s_setprio prioLevel
+    int prioLevel;                            // 1-3 (s_setprio's user priority; added to the wave's age in issue arbitration)
     // sample mode (RNG_SAMPLE): samples are summed in fixed blocks of `block` samples.  Each
     // (pixel, block) is one task, summed in sample order (fp32) by whichever lane takes it; the
     // block sum is then added to the pixel's accumulator as a 32.32 fixed-point integer
@@ -1374,10 +1375,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         accPart[threadIdx.x] = 0ull; accPart[kWave + threadIdx.x] = 0ull; accPart[2 * kWave + threadIdx.x] = 0ull;
     }
     const int lane = threadIdx.x;
-    // compat mode: all spp of a pixel in order (its per-pixel XORWOW stream).  With the pixel queue
-    // (CQ, default) persistent waves take pixels from a global counter (PT_TAKE_PIXELS): a lane
-    // whose pixel has all its samples takes the next pixel, so no lane idles while its tile's
-    // slowest pixel finishes; otherwise one wave = one tile.
+    // compat mode: all spp of a pixel in order (its per-pixel XORWOW stream).  Default: one wave =
+    // one tile (the longest tiles split, below).  The pixel queue (CQ: PT_COMPAT_QUEUE=1, an
+    // experiment, off: measured slower) makes the waves persistent and lets them
+    // take pixels from a global counter (PT_TAKE_PIXELS): a lane whose pixel has all its samples
+    // takes the next pixel.
     // sample mode: persistent waves; each lane repeatedly takes a task = (pixel, summation
     // block) from a global counter and sums that block's samples in order (see PT_TAKE_TASKS).
     // `sample` runs to nSamples (compat: spp; sample mode: the end of the task's block, and
@@ -1401,7 +1403,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     bool valid = !SAMPLE && !CQ && col < P.width && lrow < P.nrows && (slice < 0 || (lane * P.splitWays) / kWave == slice);
     uint32_t idx = valid ? (uint32_t)lrow * (uint32_t)P.width + (uint32_t)col : 0u;   // npix < 2^32
     const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
-    if (!SAMPLE && !CQ && bidT < P.prioTiles) __builtin_amdgcn_s_setprio(2);   // wave-uniform condition
+    if (!SAMPLE && !CQ && bidT < P.prioTiles) {   // wave-uniform condition (s_setprio takes an immediate)
+        if (P.prioLevel >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (P.prioLevel == 2) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+    }
     float fcol = (float)col;
     float frow = valid ? (float)globalRow(lrow, P.stripe_h, P.nparts, P.part) : 0.0f;
     const DevScene& S = P.S;
@@ -4695,8 +4701,11 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.splitWays = std::max(1, std::min(8, envCount("PT_SPLIT_WAYS", 2)));
     P.splitTiles = (lpt && f->haveOrder && !sample && !cq && kernel != PT_KERNEL_SIMPLE)
                        ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", max_depth > 16 ? 128 : 0))) : 0;
-    if (P.splitWays == 1) P.splitTiles = 0;
+    if (P.splitWays == 1 || PT_AB_NO_SPLIT) P.splitTiles = 0;   // (a build without the split prologue: grid = tiles)
     P.compatGrid = P.ntiles + P.splitTiles * (P.splitWays - 1);
+    // diagnostic: only the first k waves of the launch order (the longest tiles) -- their chains'
+    // latency with the machine otherwise idle; the other pixels are not rendered
+    if (const int lim = envCount("PT_COMPAT_GRID_LIMIT", 0)) P.compatGrid = std::min(P.compatGrid, lim);
     if (cq) {
         P.ntasks = (uint32_t)P.ntiles * 64u;   // queue slots: tile slot x 64 pixels
         if (!f->taskCounter.p && (rc = devAlloc(f->taskCounter, 64))) return rc;
@@ -4783,6 +4792,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         P.tileXY = P.tileOrder ? f->tileXY.as<uint32_t>() : f->tileXYId.as<uint32_t>();
     }
     P.prioTiles = (P.tileOrder && !sample && !cq) ? envCount("PT_PRIO_TILES", 1024) : 0;
+    P.prioLevel = std::max(1, std::min(3, envCount("PT_PRIO_LEVEL", 2)));
     if (!sample && !cq && kernel != PT_KERNEL_SIMPLE && P.ntiles > 0)   // (tile costs: atomicMax of the tile's waves)
         HIP_TRY(hipMemsetAsync(f->tileCost.p, 0, ntl * 4, st));
     DevBuf dtimes;

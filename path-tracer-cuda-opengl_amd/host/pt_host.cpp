@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <sstream>
 #include <stdexcept>
 
@@ -223,9 +224,21 @@ pt_object triangle(const point3& v0, const point3& v1, const point3& v2, int mat
     return o;
 }
 
+static size_t appendMeshes(Scene& s, const objl::Loader& ld, float scale, const vec3& t, int mat);
 size_t appendObj(Scene& s, const std::string& path, float scale, const vec3& t, int mat) {
     objl::Loader ld;
     if (!ld.LoadFile(path)) throw std::runtime_error("cannot load OBJ " + path);
+    return appendMeshes(s, ld, scale, t, mat);
+}
+// one parsed OBJ placed many times (the bunny fields): parsed once
+static const objl::Loader& loadOnce(std::unique_ptr<objl::Loader>& ld, const std::string& path) {
+    if (!ld) {
+        ld.reset(new objl::Loader());
+        if (!ld->LoadFile(path)) throw std::runtime_error("cannot load OBJ " + path);
+    }
+    return *ld;
+}
+static size_t appendMeshes(Scene& s, const objl::Loader& ld, float scale, const vec3& t, int mat) {
     size_t added = 0;
     for (const auto& m : ld.LoadedMeshes) {
         for (size_t i = 0; i + 2 < m.Indices.size(); i += 3) {
@@ -343,9 +356,10 @@ Scene buildPreset(const std::string& name, const std::string& dir, int width, in
         s.objects.push_back(sphere(point3(0, 1, 0), 1.0f, (int)s.materials.size()));
         s.materials.push_back(metal(color(0.7f, 0.6f, 0.5f), 0.0f));
         s.cam = camera(vec3(13, 2, 3), vec3(0, 0, 0), 20, aspectOf(s.width, s.height), 0, 10, 0.0f, 1.0f).abi();
-    } else if (name == "cornell" || name == "bunny_cornell" || name == "bunny_field") {
+    } else if (name == "cornell" || name == "bunny_cornell" || name == "bunny_field" || name == "bunny_field_x4") {
         if (name == "cornell") frame(800, 800, 256, 8);
         else if (name == "bunny_cornell") frame(1920, 1080, 1024, 50);
+        else if (name == "bunny_field_x4") frame(1920, 1080, 128, 16);
         else frame(1920, 1080, 512, 16);
         cornellBox(s, dir);
         const int white = 0;
@@ -355,10 +369,21 @@ Scene buildPreset(const std::string& name, const std::string& dir, int width, in
             appendObj(s, dir + "/bunny/bunny.obj", 1500.0f, vec3(438.0f, -49.96f, 113.0f), white);
         } else if (name == "bunny_field") {
             // 15 x 14 = 210 instances at x250 on the floor: 210 * 4968 + 32 = 1,043,312 triangles.
+            std::unique_ptr<objl::Loader> ld;
             for (int i = 0; i < 15; i++)
                 for (int j = 0; j < 14; j++)
-                    appendObj(s, dir + "/bunny/bunny.obj", 250.0f,
-                              vec3(24.0f + 35.5f * (float)i, -8.33f, 16.0f + 38.0f * (float)j), white);
+                    appendMeshes(s, loadOnce(ld, dir + "/bunny/bunny.obj"), 250.0f,
+                                 vec3(24.0f + 35.5f * (float)i, -8.33f, 16.0f + 38.0f * (float)j), white);
+        } else if (name == "bunny_field_x4") {
+            // C5 at 4x the triangles (an HBM-resident stress case beyond the BASELINE configs): the same
+            // floor covered by 30 x 28 = 840 half-size bunnies (x125, half the spacing),
+            // 840 * 4968 + 32 = 4,173,152 triangles -- a flattened tree and records well beyond the
+            // 256 MB Infinity Cache
+            std::unique_ptr<objl::Loader> ld;
+            for (int i = 0; i < 30; i++)
+                for (int j = 0; j < 28; j++)
+                    appendMeshes(s, loadOnce(ld, dir + "/bunny/bunny.obj"), 125.0f,
+                                 vec3(12.0f + 17.75f * (float)i, -4.165f, 8.0f + 19.0f * (float)j), white);
         }
         s.cam = camera(vec3(278, 273, -800), vec3(278, 273, 0), 40, aspectOf(s.width, s.height), 0, 10, 0.0f,
                        1.0f).abi();

@@ -147,3 +147,19 @@ def test_one_failing_rank_ends_every_rank(mode, tmp_path):
         assert "time.sleep" in out[1] or "Timeout" in out[1], out[1]
     # every rank ends within the timeout (the hung rank: its watchdog) after start-up
     assert elapsed < 120.0, elapsed
+
+
+def test_bench_method_is_the_same_at_every_n(monkeypatch):
+    """The driver divides bench.py's N = 1 and N = 8 ms_per_step: both lines must measure the same
+    method.  With the default flags every N renders one frame at a time (frames_in_flight 1) on the
+    host-built wide tree; the two-frames-in-flight figure is a separate `pipelined` field at every N."""
+    import bench
+    monkeypatch.delenv("PT_BENCH_WIDE_DEVICE", raising=False)
+    args = bench.make_parser().parse_args([])
+    got = {n: bench.run_settings(args, n) for n in (1, 2, 4, 8)}
+    assert all(v == {"frames_in_flight": 1, "wide_tree": "host"} for v in got.values()), got
+    assert not args.no_pipelined
+    monkeypatch.setenv("PT_BENCH_WIDE_DEVICE", "1")   # an override applies to every N alike
+    assert {bench.run_settings(args, n)["wide_tree"] for n in (1, 8)} == {"device"}
+    two = bench.make_parser().parse_args(["--frames-in-flight", "2"])
+    assert {bench.run_settings(two, n)["frames_in_flight"] for n in (1, 8)} == {2}

@@ -45,10 +45,11 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     """bench.py's multi-rank flow (stripe partition, per-rank RGBA8 frames, gather, un-permute,
     PNG) rehearsed with two ranks sharing the GPU over gloo: the PNG equals the 1-rank PNG, and the
     N > 1 line carries the per-rank kernel / gather figures and one frame's latency beside the
-    pipelined (two frames in flight) rate."""
+    pipelined (two frames in flight) rate; both lines report the same method (one frame at a time,
+    the host-built wide tree)."""
     import os
     import sys
-    from helpers import last_json, read_png, run_logged
+    from helpers import failure_digest, last_json, read_png, run_logged
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     common = ["bench.py", "--config", "c2", "--spp", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
               "--no-compat"]
@@ -63,8 +64,13 @@ def test_bench_two_ranks_reassemble_one_rank_frame(tmp_path):
     assert [r["rank"] for r in b["per_rank"]] == [0, 1]
     assert all(r["kernel_ms"] > 0 and r["gather_ms"] >= 0 and r["rays_per_frame"] > 0 for r in b["per_rank"])
     assert sum(r["rays_per_frame"] for r in b["per_rank"]) == b["config"]["rays_per_frame"]
-    assert b["config"]["frames_in_flight"] == 2 and b["single_frame_ms"] > 0
-    assert "[rank 1/2] phase: timed frames" in log2
+    a = last_json(log1)
+    for k in ("frames_in_flight", "wide_tree"):   # the same method at N = 1 and N = 2
+        assert a["config"][k] == b["config"][k], (k, a["config"][k], b["config"][k])
+    assert b["config"]["frames_in_flight"] == 1 and b["config"]["wide_tree"] == "host"
+    assert a["pipelined"]["frames_in_flight"] == b["pipelined"]["frames_in_flight"] == 2
+    assert b["pipelined"]["ms_per_step"] > 0 and b["pipelined"]["value"] > 0
+    assert "[rank 1/2] phase: timed frames" in log2 and "[rank 1/2] phase: pipelined frames" in log2
 
 
 @pytest.mark.timeout(400)

@@ -324,3 +324,36 @@ def test_chapter_statistic_separates_variants(orc):
     solid = [s for s in FINAL if s[1] != -0.9]
     cam = orc.camera_make((13, 2, 3), (0, 0, 0), 20.0, 1.5, 0.1, 10.0)
     assert np.abs(_blocks(orc, solid, cam, 1200, 800) - g["c13_mean"])[g["c13_consensus"]].max() > 0.1
+
+
+def test_draw_order_is_unpinned_by_block_means(pt, orc):
+    """utility.h:55-58 / 76-79 build vec3(curand_uniform()-0.5f, curand_uniform()-0.5f,
+    curand_uniform()-0.5f): C++ leaves the order in which those three draws are taken to the
+    compiler, and no reference binary or output pins what nvcc did.  The oracle (and the kernels)
+    assume x, y, z.  Reversed (z, y, x), the compat frame changes -- the same streams feed other
+    coordinates -- yet both orders pass the same statistical pins: the exp2.png block means
+    (TRIANGLEWORLD, a Lambertian + metal scene: both samplers) and the chapter-8 diffuse render
+    (randomOnUnitSphereDiscard alone).  So the pin to the reference is statistical in exactly this
+    respect: it cannot tell the two orders apart."""
+    p = pt.Preset("triangle_world", 1200, 675)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects))
+    rows = np.arange(675)
+    ref = np.load(os.path.join(GOLDEN, "exp2_blocks.npy"))
+    ch8 = np.load(os.path.join(GOLDEN, "chapter_blocks.npz"))["c8_sampleOnSphere"]
+    frames, dev = [], []
+    try:
+        for zyx in (False, True):
+            orc.set_draw_order(zyx)
+            states = orc.film_states(1, 1200, rows)
+            rgb, _ = orc.render(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), 1200, 675, rows, 4, 50,
+                                states, nthreads=os.cpu_count() or 4)
+            frames.append(rgb)
+            lin = (rgb.astype(np.float64) ** 2).reshape(27, 25, 48, 25, 3).mean(axis=(1, 3))
+            d8 = np.abs(_blocks(orc, CHAPTERS["c8_sampleOnSphere"], _chapter_camera(orc, "c8"), 1200, 600) - ch8)
+            dev.append((np.abs(lin - ref).mean(), np.abs(lin - ref).max(), d8.mean(), d8.max()))
+    finally:
+        orc.set_draw_order(False)
+    changed = (frames[0] != frames[1]).any(axis=-1).mean()
+    assert changed > 0.5, changed   # most pixels differ: the order matters to the frame
+    for e_mean, e_max, c_mean, c_max in dev:   # and neither order is rejected by the pins
+        assert e_mean < 0.006 and e_max < 0.05 and c_mean < 0.003 and c_max < 0.04, dev

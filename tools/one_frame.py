@@ -20,7 +20,7 @@ if cfg == "c5i":   # the instanced bunny field (two-level tree)
     p = ptamd.InstancedPreset("bunny_field")
     scene = ptamd.Scene.instanced(p.objects, p.mesh_first, p.mesh_count, p.instances, p.materials)
 else:
-    p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field"}[cfg])
+    p = ptamd.Preset({"c2": "cornell", "c3": "bunny_cornell", "c5": "bunny_field", "c5x4": "bunny_field_x4"}[cfg])
     scene = ptamd.Scene(p.objects, p.materials)
 film = ptamd.Film(p.width, p.height, 1, stripe_height=8, n_parts=int(os.environ.get("NPARTS", "1")),
                   part=int(os.environ.get("PART", "0")))
