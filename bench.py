@@ -295,7 +295,7 @@ def main() -> None:
 
 
 def injected(rank: int, where: str) -> str:
-    """Test hook (tests/test_gpu_bench_ranks.py): PT_BENCH_INJECT=<rank>:<where>:<kind> makes that
+    """Test hook (tests/test_gpu_zz_ranks.py): PT_BENCH_INJECT=<rank>:<where>:<kind> makes that
     rank fail at that point -- kind `raise` (an exception), `mismatch` (a frame check that fails) or
     `hang` (stops responding) -- to show that every rank then exits non-zero within the timeout."""
     spec = os.environ.get("PT_BENCH_INJECT", "")

@@ -1013,7 +1013,15 @@ struct RenderParams {
     int rawOut;                               // compat: store the raw sample sum (resolveKernel follows)
     int stripeShift, blockShift;              // log2(stripe_h), log2(block) when powers of two, else -1
     int splitTiles, splitWays;                // compat: the longest tiles run as splitWays waves each
-    int compatGrid;                           // compat (tile waves): ntiles + splitTiles * (splitWays - 1)
+    int compatGrid;                           // compat (tile waves): critWaves + ntiles + splitTiles * (splitWays - 1)
+    // compat, critical pixels (wide kernel): the nCrit pixels of critList (the previous launch's
+    // longest chains) run first, critLanes per wave (blocks 0 .. critWaves - 1), each lane taking its
+    // pixel's whole chain with a per-lane closest-hit traversal inside the ray start (no NODE / LEAF
+    // steps); tile waves skip the pixels critFlag marks.  pixRays (optional): rays per pixel.
+    int nCrit, critLanes, critWaves;
+    const uint32_t* critList;
+    const uint8_t* critFlag;
+    uint32_t* pixRays;
 };
 
 // (blockFixed, blockFixedSmall, fixedToFloat: pt_math.hpp)
@@ -1021,6 +1029,20 @@ struct RenderParams {
 // that measure tile costs (`cost`: the input of the next launches' longest-first order) -- its ray
 // count; no-return atomics (device scope: 4 of them per task cost 5 % of a C3 frame, so the ray
 // counts are taken on one frame in eight).
+// compat critical pixels: how many (PT_CRIT_PIXELS) and how many per wave (PT_CRIT_LANES)
+#ifndef PT_CRIT_PIXELS
+#define PT_CRIT_PIXELS 1024
+#endif
+#ifndef PT_CRIT_LANES
+#define PT_CRIT_LANES 8
+#endif
+constexpr int kCritPixels = PT_CRIT_PIXELS;
+constexpr int kCritLanes = PT_CRIT_LANES;
+// which compat kernels have critical-pixel waves: the flattened wide tree on shallow trees (stack 8:
+// the 4-waves/SIMD compat kernels, whose 128-VGPR budget holds the per-lane loop without spills)
+__host__ __device__ constexpr bool critFor(bool sample, bool wide, bool inst, bool cq, int stack) {
+    return !sample && wide && !inst && !cq && stack <= 8;
+}
 __device__ __forceinline__ __attribute__((unused)) void addFixed1(unsigned long long* acc, unsigned long long v) {
 #if PT_AB_NO_ATOMICS
     return;
@@ -1389,21 +1411,39 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // of 64 / splitWays pixels per wave (the other lanes idle), so a critical pixel shares its wave's
     // steps with fewer other pixels and its chain advances in more of them.
     int bidT = (int)blockIdx.x, slice = -1;
+    // compat, critical-pixel waves (CRIT): the first critWaves blocks (wave-uniform)
+    constexpr bool CRITK = critFor(SAMPLE, WIDE, INST, CQ, STACK);
+    const bool crit = CRITK && bidT < P.critWaves;
+    if constexpr (CRITK) {
+        if (!crit) bidT -= P.critWaves;
+    }
     if constexpr (!SAMPLE && !CQ && !PT_AB_NO_SPLIT) {
         const int ks = P.splitTiles * P.splitWays;   // (uniform)
-        if (bidT < ks) { slice = bidT % P.splitWays; bidT /= P.splitWays; }
+        if (crit) {
+        } else if (bidT < ks) { slice = bidT % P.splitWays; bidT /= P.splitWays; }
         else bidT -= ks - P.splitTiles;
     }
-    int tile = (SAMPLE || CQ) ? -1 : tileOf(P, bidT), nSamples = SAMPLE ? 0 : P.spp;
+    int tile = (SAMPLE || CQ || crit) ? -1 : tileOf(P, bidT), nSamples = SAMPLE ? 0 : P.spp;
     int col = 0, lrow = 0;
+    bool valid = false;
+    uint32_t idx = 0u;
     if constexpr (!SAMPLE && !CQ) {
-        col = (tile % P.tiles_x) * 8 + (lane & 7);
-        lrow = (tile / P.tiles_x) * 8 + (lane >> 3);
+        if (crit) {   // a listed pixel per lane (lanes beyond critLanes or the list idle)
+            const int k = bidT * P.critLanes + lane;
+            valid = lane < P.critLanes && k < P.nCrit;
+            idx = valid ? P.critList[k] : 0u;
+            col = (int)(idx % (uint32_t)P.width);
+            lrow = (int)(idx / (uint32_t)P.width);
+        } else {
+            col = (tile % P.tiles_x) * 8 + (lane & 7);
+            lrow = (tile / P.tiles_x) * 8 + (lane >> 3);
+            valid = col < P.width && lrow < P.nrows && (slice < 0 || (lane * P.splitWays) / kWave == slice);
+            idx = valid ? (uint32_t)lrow * (uint32_t)P.width + (uint32_t)col : 0u;   // npix < 2^32
+            if (CRITK && valid && P.critFlag && P.critFlag[idx]) valid = false;   // (a critical wave's pixel)
+        }
     }
-    bool valid = !SAMPLE && !CQ && col < P.width && lrow < P.nrows && (slice < 0 || (lane * P.splitWays) / kWave == slice);
-    uint32_t idx = valid ? (uint32_t)lrow * (uint32_t)P.width + (uint32_t)col : 0u;   // npix < 2^32
     const unsigned long long tStart = __builtin_amdgcn_s_memrealtime();
-    if (!SAMPLE && !CQ && bidT < P.prioTiles) {   // wave-uniform condition (s_setprio takes an immediate)
+    if (!SAMPLE && !CQ && !crit && bidT < P.prioTiles) {   // wave-uniform condition (s_setprio takes an immediate)
         if (P.prioLevel >= 3) __builtin_amdgcn_s_setprio(3);
         else if (P.prioLevel == 2) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
@@ -1451,6 +1491,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     bool active = false;
     // sample mode task state: summation block, its tile (cost accounting), rays traced for it
     uint32_t depthPaths = 0;
+    uint32_t pxRays = 0;   // compat tile / critical lanes: rays traced for the lane's pixel (P.pixRays)
     bool needTask = SAMPLE || CQ;
     uint32_t poolBase = 0u, poolLeft = 0u;   // sample mode / CQ: the wave's reserved tasks (uniform)
 
@@ -1472,6 +1513,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         best = -1;                                                                                \
         sp = 0;                                                                                   \
         qn = 0;                                                                                   \
+        if constexpr (CRITK) pxRays++;                                                            \
         if constexpr (WIDE) {   /* the root is slot 0 of a virtual node at base 0 */              \
             if (PT_AB_CHEAP_START) inv = f3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z)); \
             else inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                    \
@@ -1492,6 +1534,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 const auto& K_ = *kargs();                                                        \
                 (void)instEntry(K_.S.cx, K_.S.cy, K_.S.cz, K_.S.ext, o, d, inv);                   \
             }                                                                                     \
+            if (CRITK && crit) PT_CRIT_TRACE();                                                    \
         } else if (S.nprims <= 1) {                                                               \
             node = -1;                                                                            \
             if (S.nprims == 1) { /* root is a leaf: no box test (render_manager.h:92-98) */       \
@@ -1503,6 +1546,51 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
             inv = f3(rcpRN(d.x), rcpRN(d.y), rcpRN(d.z));                                         \
             node = 0;                                                                             \
         }                                                                                         \
+    } while (0)
+    // Critical-pixel waves (compat, wide): the lane's whole closest-hit query at once, in a per-lane
+    // loop (nearest child first, the NODE and LEAF steps' own tests and tie / window rules, no
+    // speculation): a lane alone on its chain advances every iteration instead of waiting for the
+    // wave's step kinds.  The result is the reference's closest hit either way;
+    // a flagged order-dependent query is redone in the reference's order by the SHADE step as usual.
+#define PT_CRIT_TRACE()                                                                             \
+    do {                                                                                          \
+        const bool lb_ = S.nprims > 1;                                                            \
+        const bool sph_ = kargs()->S.hasSpheres != 0;                                             \
+        bool redo_ = false;                                                                       \
+        for (;;) {                                                                                \
+            while (tg) {                                                                          \
+                const uint32_t k_ = tgBase + (uint32_t)__builtin_ctz(tg);                         \
+                tg &= tg - 1u;                                                                    \
+                const float4* w_ = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(S.wprims) + mul48(k_)); \
+                const Prim q_{w_[0], w_[1], w_[2]};                                               \
+                const bool isS_ = __float_as_uint(q_.p2.w) != 0u;                                 \
+                sTris += (uint32_t)__popcll(__ballot(!isS_));                                     \
+                sSph += (uint32_t)__popcll(__ballot(isS_));                                       \
+                if (sph_) wideTest<true>(q_, o, d, inv, 0.001f, closest, best, bestLo, lb_, redo_, 0u); \
+                else wideTest<false>(q_, o, d, inv, 0.001f, closest, best, bestLo, lb_, redo_, 0u); \
+            }                                                                                     \
+            if ((ng & 0xffu) == 0u) {                                                             \
+                if (sp == 0) break;                                                               \
+                sp--;                                                                             \
+                ng = my[sp * kWave];                                                              \
+            }                                                                                     \
+            const uint32_t bit_ = (uint32_t)__builtin_ctz(ng & 0xffu);                            \
+            const uint32_t child_ = (ng >> 8) + (bit_ ^ (oct & 7u));                              \
+            ng &= ~(1u << bit_);                                                                  \
+            if (ng & 0xffu) { my[sp * kWave] = ng; sp++; }   /* sp < depth <= STACK (host check) */ \
+            sVisits += (uint32_t)__popcll(__ballot(true));                                        \
+            const uint32_t off_ = mul80(child_);                                                  \
+            const uint4 n0_ = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off_, 0, 0)); \
+            const uint4 n1_ = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off_ + 16u, 0, 0)); \
+            const uint4 n2_ = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off_ + 32u, 0, 0)); \
+            const uint4 n3_ = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off_ + 48u, 0, 0)); \
+            const uint4 n4_ = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(nodeRsrc, off_ + 64u, 0, 0)); \
+            const uint32_t h_ = wideHits<PT_WIDE_MIX != 0>(n0_, n1_, n2_, n3_, n4_, o, inv, oct & 7u, 0.001f, closest); \
+            ng = (n1_.x << 8) | (h_ >> 24);                                                      \
+            tgBase = n1_.y;                                                                       \
+            tg = h_ & 0xffffffu;                                                                  \
+        }                                                                                         \
+        if (redo_) oct |= 8u;   /* order-dependent candidate: SHADE repeats the query */           \
     } while (0)
     // New camera sample: main.cu:284-286 + camera::get_ray (lens sample: lensOffset; time draw skipped).
     // Sample mode: lanes with needTask take the next tasks of the wave's pool, in lane order; an
@@ -2243,13 +2331,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
         if (valid) {
             storePixel(P, idx, sum);
             P.sd[idx] = g.d; P.s0[idx] = g.v0; P.s1[idx] = g.v1; P.s2[idx] = g.v2; P.s3[idx] = g.v3; P.s4[idx] = g.v4;
+            if (CRITK && P.pixRays) P.pixRays[idx] = pxRays;   // (the next launch's critical pixels)
         }
     }
     const unsigned long long tEnd = __builtin_amdgcn_s_memrealtime();
 #if PT_AB_COST_STORE
-    if (!SAMPLE && !CQ && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
+    if (!SAMPLE && !CQ && !crit && lane == 0) P.tileCost[tile] = (unsigned)min(tEnd - tStart, 0xffffffffull);
 #else
-    if (!SAMPLE && !CQ && lane == 0) atomicMax(P.tileCost + tile, (unsigned)min(tEnd - tStart, 0xffffffffull));   // (split tiles: several waves)
+    if (!SAMPLE && !CQ && !crit && lane == 0) atomicMax(P.tileCost + tile, (unsigned)min(tEnd - tStart, 0xffffffffull));   // (split tiles: several waves)
 #endif
     if constexpr (SAMPLE) {   // max_depth <= 0: paths counted per lane
 
@@ -2292,6 +2381,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     }
 }
 #undef PT_BEGIN_RAY
+#undef PT_CRIT_TRACE
 #undef PT_NEW_PATH
 #undef PT_TAKE_TASKS
 #undef PT_FINISH_TASK
@@ -2400,6 +2490,12 @@ __global__ __launch_bounds__(256) void tileXYKernel(const uint32_t* __restrict__
     const uint32_t t = order ? order[i] : (uint32_t)i;
     const uint32_t ty = t / (uint32_t)tilesX;
     xy[i] = (t - ty * (uint32_t)tilesX) | (ty << 16);
+}
+
+// compat: mark the next launch's critical pixels (the first k of the pixels sorted by rays)
+__global__ __launch_bounds__(256) void critFlagKernel(const uint32_t* __restrict__ sorted, int k, uint8_t* flag) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) flag[sorted[i]] = 1;
 }
 
 __global__ __launch_bounds__(256) void tileKeyKernel(const unsigned* __restrict__ cost, uint32_t* keys, uint32_t* ids,
@@ -3333,6 +3429,10 @@ struct pt_film {
     bool haveOrder = false;
     int framesSinceCost = 0;      // sample mode: frames rendered since the tile costs were last measured
     DevBuf pixAcc, taskCounter;   // sample mode: per-pixel {x, y, z, rays} accumulators; task counter
+    // compat mode, wide kernel: rays per pixel of the last launch, and the next launch's critical
+    // pixels (the longest chains: their ids sorted by descending rays, and a flag per pixel)
+    DevBuf pixRays, pixKeys, pixKeys2, pixIds, pixSorted, critFlag, critTemp;
+    int critK = 0;                // critical pixels selected for the next compat launch (0: none yet)
     DevBuf stackSpill;            // sample mode on deep trees: traversal stack entries beyond LDS
     DevBuf sums;                  // compat mode: raw per-pixel sample sums of the frame (resolve input)
     DevBuf accum;                 // progressive rendering: fp32 RGB running sums of every accumulated frame
@@ -4702,7 +4802,28 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     P.splitTiles = (lpt && f->haveOrder && !sample && !cq && kernel != PT_KERNEL_SIMPLE)
                        ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", max_depth > 16 ? 128 : 0))) : 0;
     if (P.splitWays == 1 || PT_AB_NO_SPLIT) P.splitTiles = 0;   // (a build without the split prologue: grid = tiles)
-    P.compatGrid = P.ntiles + P.splitTiles * (P.splitWays - 1);
+    // compat critical pixels (wide kernel, flattened scene): the previous launch's longest per-pixel
+    // chains run first, PT_CRIT_LANES pixels per wave, each lane tracing its rays in one per-lane loop
+    // (a lane alone on its chain is not held back by the wave's step kinds); measured per launch
+    P.nCrit = 0;
+    P.critLanes = std::max(1, std::min(64, envCount("PT_CRIT_LANES", kCritLanes)));
+    P.critWaves = 0;
+    P.critList = nullptr;
+    P.critFlag = nullptr;
+    P.pixRays = nullptr;
+    const bool critOn = lpt && critFor(sample, kernel == PT_KERNEL_WIDE, s->instanced, cq, stack) && np > 0 &&
+                        max_depth > 16 && envCount("PT_CRIT_PIXELS", kCritPixels) > 0;
+    if (critOn) {
+        if ((rc = devReserve(f->pixRays, (size_t)np * 4))) return rc;
+        P.pixRays = f->pixRays.as<uint32_t>();
+        if (f->critK > 0) {
+            P.nCrit = f->critK;
+            P.critWaves = (P.nCrit + P.critLanes - 1) / P.critLanes;
+            P.critList = f->pixSorted.as<uint32_t>();
+            P.critFlag = f->critFlag.as<uint8_t>();
+        }
+    }
+    P.compatGrid = P.critWaves + P.ntiles + P.splitTiles * (P.splitWays - 1);
     // diagnostic: only the first k waves of the launch order (the longest tiles) -- their chains'
     // latency with the machine otherwise idle; the other pixels are not rendered
     if (const int lim = envCount("PT_COMPAT_GRID_LIMIT", 0)) P.compatGrid = std::min(P.compatGrid, lim);
@@ -4859,6 +4980,28 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
             std::fprintf(stderr, "[pt] tile order check: %zu tiles, %zu out of range, %zu duplicates, %zu unsorted pairs\n",
                          ntl, bad, dup, unsorted);
         }
+    }
+    if (critOn) {   // the next launch's critical pixels: the K longest chains of this one (a stable radix sort)
+        const int64_t K = std::min<int64_t>(envCount("PT_CRIT_PIXELS", kCritPixels), np);
+        const size_t n = (size_t)np;
+        if ((rc = devReserve(f->pixKeys, n * 4)) || (rc = devReserve(f->pixKeys2, n * 4)) ||
+            (rc = devReserve(f->pixIds, n * 4)) || (rc = devReserve(f->pixSorted, n * 4)) ||
+            (rc = devReserve(f->critFlag, n)))
+            return rc;
+        size_t cbytes = 0;
+        HIP_TRY(pt::radixSortPairs(nullptr, &cbytes, f->pixKeys.as<uint32_t>(), f->pixKeys2.as<uint32_t>(),
+                                   f->pixIds.as<uint32_t>(), f->pixSorted.as<uint32_t>(), n, 32, st));
+        if ((rc = devReserve(f->critTemp, cbytes))) return rc;
+        tileKeyKernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(f->pixRays.as<unsigned>(), f->pixKeys.as<uint32_t>(),
+                                                                  f->pixIds.as<uint32_t>(), (int)n);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(pt::radixSortPairs(f->critTemp.p, &cbytes, f->pixKeys.as<uint32_t>(), f->pixKeys2.as<uint32_t>(),
+                                   f->pixIds.as<uint32_t>(), f->pixSorted.as<uint32_t>(), n, 32, st));
+        HIP_TRY(hipMemsetAsync(f->critFlag.p, 0, n, st));
+        critFlagKernel<<<(unsigned)((K + 255) / 256), 256, 0, st>>>(f->pixSorted.as<uint32_t>(), (int)K,
+                                                                   f->critFlag.as<uint8_t>());
+        HIP_TRY(hipGetLastError());
+        f->critK = (int)K;
     }
     if (P.waveTimes) {
         HIP_TRY(hipStreamSynchronize(st));

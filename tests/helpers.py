@@ -158,7 +158,24 @@ def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
     if log_path is None:
         log_path = tempfile.mktemp(suffix=".log")
     t0 = time.perf_counter()
+    # every multi-process log is kept as evidence (PT_TEST_LOG_DIR, default gpurun_out/test_logs/:
+    # the scratch directory a GPU box's results come back in)
+    keep = os.environ.get("PT_TEST_LOG_DIR") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "test_logs")
+
+    def kept(text, rc):
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            name = os.path.basename(os.path.dirname(str(log_path))) + "_" + os.path.basename(str(log_path))
+            with open(os.path.join(keep, name), "w") as f:
+                f.write(text + f"\n[run_logged] rc={rc} wall={time.perf_counter() - t0:.1f} s\n")
+        return text
+
     with open(log_path, "w+") as log:
+        # the parent's situation when the child starts: its own GPU state and the box's load
+        log.write(f"[run_logged] parent pid {os.getpid()}: loadavg {os.getloadavg()}, "
+                  f"parent GPU context {'yes' if _parent_gpu_state() else 'no'}\n")
+        log.flush()
         p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
         try:
             rc = p.wait(timeout=timeout)
@@ -170,9 +187,17 @@ def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
             p.wait()
             log.seek(0)
             raise AssertionError(f"{' '.join(map(str, cmd[:8]))} ... still running after {timeout} s; log tail:\n"
-                                 + log.read()[-4000:])
+                                 + kept(log.read(), "timeout")[-4000:])
         log.seek(0)
-        return rc, log.read(), time.perf_counter() - t0
+        return rc, kept(log.read(), rc), time.perf_counter() - t0
+
+
+def _parent_gpu_state():
+    """Whether this (pytest) process has created GPU state: torch initialised CUDA/HIP, or libpt
+    (ptamd) was imported (its films and scenes hold device memory and streams)."""
+    import sys
+    t = sys.modules.get("torch")
+    return bool((t is not None and t.cuda.is_initialized()) or "ptamd" in sys.modules)
 
 
 def failure_digest(text, tail=2500):

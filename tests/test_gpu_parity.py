@@ -547,3 +547,48 @@ def test_compat_split_tiles_bit_exact(pt, orc, gpu, monkeypatch, kname, ways):
             np.testing.assert_array_equal(bits(rgb), bits(ref))
             assert st.rays == rst.rays and st.paths == w * h * spp
             np.testing.assert_array_equal(f.get_rng(), ref_states)
+
+
+@pytest.mark.parametrize("crit,lanes", [("1", "1"), ("100", "8"), ("100000", "64"), ("37", "3")])
+def test_compat_critical_pixels_bit_exact(pt, orc, gpu, monkeypatch, crit, lanes):
+    """Compat mode's critical pixels (the wide kernel on shallow trees, long paths): launches after
+    the first take the previous launch's PT_CRIT_PIXELS longest per-pixel chains out of the tile
+    waves and run them first, PT_CRIT_LANES per wave, each lane tracing its rays in one per-lane
+    loop.  Every launch's frame, advanced RNG streams and counters equal the oracle's -- with one
+    critical pixel, some, every pixel of the frame, and ragged waves."""
+    monkeypatch.setenv("PT_CRIT_PIXELS", crit)
+    monkeypatch.setenv("PT_CRIT_LANES", lanes)
+    w, h, spp, depth = 72, 40, 3, 50
+    p = pt.Preset("bunny_cornell", w, h)
+    s = pt.Scene(p.objects, p.materials, device=gpu)
+    nodes = orc.build_lbvh(p.objects, orc.morton_keys(p.objects), tight=True)
+    f = pt.Film(w, h, 6, device=gpu)
+    ref_states = orc.film_states(6, w, f.rows)
+    ref, rst = orc.render(p.objects, p.materials, nodes, pt.camera_to_array(p.camera), w, h, f.rows, spp, depth,
+                          ref_states, nthreads=8)
+    for _ in range(3):   # (the first launch measures the chains; later ones run the critical pixels first)
+        f.reset()
+        rgb, st = pt.render(s, f, p.camera, spp, depth, kernel=pt.KERNEL_WIDE)
+        np.testing.assert_array_equal(bits(rgb), bits(ref))
+        assert st.rays == rst.rays and st.paths == w * h * spp
+        assert st.tri_tests > 0 and st.node_visits > 0   # (the wide tree's own counts, not the oracle's)
+        np.testing.assert_array_equal(f.get_rng(), ref_states)
+    # accumulating frames (raw sums through the resolve pass) and 8-bit output take the same path
+    f.reset()
+    f.clear()
+    a, _ = pt.render(s, f, p.camera, spp, depth, kernel=pt.KERNEL_WIDE, accumulate=True)
+    np.testing.assert_array_equal(bits(a), bits(ref))
+
+
+@pytest.mark.parametrize("spp,chunk", [(128, 16), (96, 4)])
+def test_sample_mode_repeated_launches_bit_exact(pt, orc, gpu, spp, chunk):
+    """Sample mode on several launches of one film (the first measures tile costs, then frames
+    without them and, every 8th, with them again): every frame of the wide kernel equals the oracle."""
+    w, h, depth = 48, 40, 50
+    p = pt.Preset("bunny_cornell", w, h)
+    rgb, st, ref, rst, s, f = render_sample_both(pt, orc, gpu, p, w, h, spp, depth, 5, chunk)
+    np.testing.assert_array_equal(bits(rgb), bits(ref))
+    for _ in range(9):
+        again, ast = pt.render(s, f, p.camera, spp, depth, rng=pt.RNG_SAMPLE, chunk=chunk, kernel=pt.KERNEL_WIDE)
+        np.testing.assert_array_equal(bits(again), bits(ref))
+        assert ast.rays == rst.rays

@@ -3,11 +3,11 @@ over ranks, the gather to rank 0 and the un-permuted PNG equal to the 1-rank PNG
 the box's one GPU, and RCCL with the one rank a one-GPU box allows), the fail-fast of a failing
 rank, and the C4 8-rank rehearsal.
 
-These tests start their own GPU processes (up to 8 ranks).  They live in a file of their own that
-sorts first among the GPU tests, so they run before the suite's own process has created any GPU
-state: after ~300 in-process tests the same 8-rank rehearsal took 171 s instead of 39 s with the
-suite process's GPU context alive beside its ranks (not pinned down further; the rehearsal's
-timeouts leave room for either).
+These tests start their own GPU processes (up to 8 ranks).  The file sorts LAST among the GPU
+tests (round 6; in round 5 it ran first): the ranks then share the GPU with the suite process, which
+by then holds its own GPU context, streams and device memory -- the order in which the 8-rank
+rehearsal once failed (round 5, gpurun_out/r05h).  Each run's log records whether the parent holds
+GPU state and the box's load, and with PT_TEST_LOG_DIR set every log is kept (helpers.run_logged).
 """
 import numpy as np
 import pytest
@@ -135,7 +135,7 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     """C4 (BASELINE.json configs[3]: the C3 scene at 1920x1080, 4096 spp, row-tiled over 8 GPUs)
     through bench.py's own multi-rank flow: 8 ranks over gloo sharing this one GPU (a rehearsal,
     never a reported number), each rendering its 1/8 of the stripes at the full sample count on the
-    wide tree its own device built; the gathered, un-permuted PNG equals the 1-rank PNG byte for
+    wide tree it built (host SAH, as at N = 1); the gathered, un-permuted PNG equals the 1-rank PNG byte for
     byte and the rank-0 line reports the whole frame's rays and all eight ranks' figures."""
     import os
     import sys
@@ -158,7 +158,9 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     l1, l8 = last_json(log1), last_json(log8)
     assert l1["config"]["spp"] == l8["config"]["spp"] == 4096 and l8["n_gpus"] == 8
     assert l1["config"]["rays_per_frame"] == l8["config"]["rays_per_frame"] > 4 * 1920 * 1080 * 4096
-    assert len(l8["per_rank"]) == 8 and "lbvh_plus_wide_tree_device_ms" in l8["scene_build"]
+    assert len(l8["per_rank"]) == 8 and "wide_tree_host_ms" in l8["scene_build"]
+    assert l1["config"]["wide_tree"] == l8["config"]["wide_tree"] == "host"   # one method at N = 1 and N = 8
+    assert l1["config"]["frames_in_flight"] == l8["config"]["frames_in_flight"] == 1
 
 
 @pytest.mark.timeout(200)

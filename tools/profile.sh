@@ -2,7 +2,8 @@
 # Bench + rocprofv3 session on the GPU box (run via gpurun).  TAG names the output dir.
 #  1. python bench.py (the driver's default command)          -> gpurun_out/$TAG/bench.json
 #  2. rocprofv3 --kernel-trace --stats of the same frames (without the CPU baseline and the
-#     interactive-mode frames, whose 1-16 spp launches would mix into the render kernel's average)
+#     interactive-mode frames, whose 1-16 spp launches would mix into the render kernel's average,
+#     and without the `pipelined` frames, whose overlapping launches last longer than a frame)
 #                                                               -> gpurun_out/$TAG/trace/
 #  3. separate --pmc passes (FETCH_SIZE | WRITE_SIZE | TCC hit/miss | SQ | VALU instructions) on one frame
 set -o pipefail
@@ -12,8 +13,8 @@ TAG=${TAG:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 BENCH_ARGS=${BENCH_ARGS:-}
-PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-compat --no-interactive}
-TRACE_ARGS=${TRACE_ARGS:---no-cpu-baseline --no-interactive}
+PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-compat --no-interactive --no-pipelined}
+TRACE_ARGS=${TRACE_ARGS:---no-cpu-baseline --no-interactive --no-pipelined}
 step() {  # name, limit, command...
     local name=$1 lim=$2; shift 2
     timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1
