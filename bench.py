@@ -451,7 +451,10 @@ def run(args, world: int, rank: int, local: int, backend: str, dev, dist_on: boo
         st1 = frame(1, wait=True)   # (film 1's first launch: its tile costs for the launch order)
         check(st1, 1, "warmup frames")
         warm_kms = st1.kernel_ms
-    for k in range(max(0, args.warmup - 1)):
+    # (the reference-order frame above counts as one warmup step; the benchmarked kernel gets at least
+    # one warmup frame of its own, so its first use -- the wide tree's host build, module loading --
+    # never falls into the timed region)
+    for k in range(max(1, args.warmup - 1) if args.warmup > 0 else 0):
         stw = frame(k % fif, wait=True)
         check(stw, k % fif, "warmup frames")
         warm_kms = stw.kernel_ms

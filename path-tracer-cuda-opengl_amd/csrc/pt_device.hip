@@ -1031,10 +1031,10 @@ struct RenderParams {
 // counts are taken on one frame in eight).
 // compat critical pixels: how many (PT_CRIT_PIXELS) and how many per wave (PT_CRIT_LANES)
 #ifndef PT_CRIT_PIXELS
-#define PT_CRIT_PIXELS 1024
+#define PT_CRIT_PIXELS 256
 #endif
 #ifndef PT_CRIT_LANES
-#define PT_CRIT_LANES 8
+#define PT_CRIT_LANES 4
 #endif
 constexpr int kCritPixels = PT_CRIT_PIXELS;
 constexpr int kCritLanes = PT_CRIT_LANES;
@@ -3586,6 +3586,32 @@ void meshSubRoots(const pt::Wide8& w, uint32_t slot, const double* box, int leve
     for (const SubRoot& c : ch) meshSubRoots(w, c.slot, c.box, levels - 1, out);
 }
 
+// Partial re-braiding chosen by surface area (PT_INST_ENTRIES = k > 0): start from the root's
+// internal children and repeatedly open the entry of the largest surface area (a node whose children
+// are all internal) while the entries stay within k per instance -- the large, overlapping boxes are
+// opened, the small ones stay closed (in the spirit of Benthin et al. 2017's SAH-driven re-braiding).
+void meshSubRootsBudget(const pt::Wide8& w, size_t budget, std::vector<SubRoot>& out) {
+    out = nodeChildren(w, 0u);
+    if (out.empty()) return;
+    auto area = [](const SubRoot& r) {
+        const double x = r.box[3] - r.box[0], y = r.box[4] - r.box[1], z = r.box[5] - r.box[2];
+        return x * y + y * z + z * x;
+    };
+    std::vector<bool> closed(out.size(), false);
+    for (;;) {
+        int pick = -1;
+        double best = -1.0;
+        for (size_t i = 0; i < out.size(); i++)
+            if (!closed[i] && area(out[i]) > best) { best = area(out[i]); pick = (int)i; }
+        if (pick < 0) break;
+        std::vector<SubRoot> ch = nodeChildren(w, out[(size_t)pick].slot);
+        if (ch.empty() || out.size() - 1 + ch.size() > budget) { closed[(size_t)pick] = true; continue; }
+        out.erase(out.begin() + pick);
+        closed.erase(closed.begin() + pick);
+        for (const SubRoot& c : ch) { out.push_back(c); closed.push_back(false); }
+    }
+}
+
 float mixLimit(double m);   // (below)
 
 int buildInstanced(pt_scene* s) {
@@ -3780,7 +3806,9 @@ int buildInstanced(pt_scene* s) {
     std::vector<std::vector<SubRoot>> sub((size_t)nm);
     for (int m = 0; m < nm; m++) {
         const double inf[6] = {-INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, INFINITY};
-        if (rebraid > 0) meshSubRoots(blas[(size_t)m], 0u, inf, rebraid, sub[(size_t)m]);
+        const int budget = envCount("PT_INST_ENTRIES", 0);   // (A/B: surface-area-chosen partial re-braiding)
+        if (budget > 0) meshSubRootsBudget(blas[(size_t)m], (size_t)budget, sub[(size_t)m]);
+        else if (rebraid > 0) meshSubRoots(blas[(size_t)m], 0u, inf, rebraid, sub[(size_t)m]);
         if (sub[(size_t)m].size() == 1) sub[(size_t)m].clear();   // (the root itself)
     }
     std::vector<InstEntry> entries;
@@ -4739,14 +4767,19 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         P.camFar = !(m <= (s->wideSource == 3 ? (double)kInstFarExt : 8.0) * (double)s->sceneCE[3]) ? 1 : 0;
     }
     // Defaults swept on C3 (tools/ab_env.py): sample mode is throughput-bound and prefers full
-    // LEAF / SHADE steps.  Compat mode is bound by its slowest pixels' sequential chains: 20 / 12
-    // together with nodeMin 8 (C3 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 -> 1,180 against 8 / 12).
+    // LEAF / SHADE steps.  Compat mode on the binary tree is bound by its slowest pixels' sequential
+    // chains: 20 / 12 together with nodeMin 8 (C3 1,521 -> 1,442 ms, C2 90.7 -> 80.0, C5 1,311 ->
+    // 1,180 against 8 / 12).  Compat on the flattened wide tree, since round 6 (its critical chains
+    // in critical-pixel waves, or short paths): the sample mode's wide thresholds with nodeMin 8 --
+    // C3 @1024 (critical pixels on) 705 -> 649 ms (SHADE 28 alone 665, 20 674; LEAF 28 alone 695),
+    // C5 @512 558 -> 539 (24 / 24), C2 @256 37.7 -> 37.1; nodeMin 0 740 / 617 ms, 4: 656 on C3.
     const bool sampleRng = rng == PT_RNG_SAMPLE;
     // sample mode, wide kernel (speculative traversal): LEAF at 28 waiting lanes, SHADE at 28
     // (C3 @256 spp 148.4 -> 145.0 ms vs 24 / 32; C5 @64 75.9 -> 74.5; C2 @1024 135.4 -> 134.5);
     // deep wide trees (a 16+ entry stack: C5's 1.04 M triangles) at 24 / 24 (round 3 close: C5 @64
     // 67.1 -> 65.1 ms, median of 5; C3 at 24 / 24 is 1 % slower, so shallow trees keep 28 / 28)
     const bool wideSample = sampleRng && kernel == PT_KERNEL_WIDE;
+    const bool wideFlatCompat = !sampleRng && kernel == PT_KERNEL_WIDE && !s->instanced;
     const int stack = kernel == PT_KERNEL_WIDE ? wideStackFor(s->wideDepth) : (s->nobj > 1 ? stackFor(s->depth) : 16);
     const int wideBatch = stack >= 16 ? 24 : 28;
     // instanced scenes (no speculative traversal: a lane with primitives waiting cannot visit nodes)
@@ -4754,12 +4787,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     // median of 3: 131.8 -> 128.8 ms; LEAF 12: 131.8, 8: 135.9, 32: 140.7; SHADE 28 with LEAF 16: 131.4)
     const bool instSample = wideSample && s->instanced;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
-                                                 : envInt("PT_LEAF_BATCH", instSample ? 16 : wideSample ? wideBatch : (sampleRng ? 24 : 20));
+                                                 : envInt("PT_LEAF_BATCH", instSample ? 16 : (wideSample || wideFlatCompat) ? wideBatch
+                                                                                                       : (sampleRng ? 24 : 20));
     // compat mode: a NODE step with fewer than nodeMin lanes yields to the larger of the waiting
     // LEAF / SHADE groups (C3 compat 1,620 -> 1,517 ms at 8; 4: 1,548, 16: 1,671, 32: 1,989)
     P.nodeMin = std::getenv("PT_NODE_MIN") ? std::atoi(std::getenv("PT_NODE_MIN")) : 8;
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
-                                                   : envInt("PT_SHADE_BATCH", instSample ? 20 : wideSample ? wideBatch : (sampleRng ? 32 : 12));
+                                                   : envInt("PT_SHADE_BATCH", instSample ? 20 : (wideSample || wideFlatCompat) ? wideBatch
+                                                                                                           : (sampleRng ? 32 : 12));
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
     const size_t ntl = (size_t)std::max(1, P.ntiles);
     if (!f->tileCost.p) {
@@ -4794,17 +4829,12 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if (c) c->store(perCU, std::memory_order_relaxed);
         return PT_OK;
     };
-    // compat tile waves: the longest tiles of the launch order split into splitWays waves (renderKernelWF).
-    // Only where a pixel's sequential chain can outlast the frame's throughput-bound part: long paths
-    // (max_depth > 16; C3, depth 50: 800 -> 766 ms).  Short-path frames are throughput-bound and the
-    // split's idle lanes cost (C5, depth 16: 548 -> 553 ms; C2, depth 8: +0.9 %).
-    P.splitWays = std::max(1, std::min(8, envCount("PT_SPLIT_WAYS", 2)));
-    P.splitTiles = (lpt && f->haveOrder && !sample && !cq && kernel != PT_KERNEL_SIMPLE)
-                       ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", max_depth > 16 ? 128 : 0))) : 0;
-    if (P.splitWays == 1 || PT_AB_NO_SPLIT) P.splitTiles = 0;   // (a build without the split prologue: grid = tiles)
-    // compat critical pixels (wide kernel, flattened scene): the previous launch's longest per-pixel
-    // chains run first, PT_CRIT_LANES pixels per wave, each lane tracing its rays in one per-lane loop
-    // (a lane alone on its chain is not held back by the wave's step kinds); measured per launch
+    // compat critical pixels (wide kernel, flattened scene, long paths): the previous launch's
+    // PT_CRIT_PIXELS longest per-pixel chains run first, PT_CRIT_LANES pixels per wave, each lane
+    // tracing its rays in one per-lane loop (a lane alone on its chain is not held back by the wave's
+    // step kinds).  C3 compat @1024 (interleaved, median of 2): 773 ms without; 256 x 4 699 ms;
+    // 64 x 1 710, 128 x 4 707, 512 x 4 712, 256 x 8 751 (with the split tiles as well).  The rays
+    // per pixel are measured on every launch.
     P.nCrit = 0;
     P.critLanes = std::max(1, std::min(64, envCount("PT_CRIT_LANES", kCritLanes)));
     P.critWaves = 0;
@@ -4823,6 +4853,16 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
             P.critFlag = f->critFlag.as<uint8_t>();
         }
     }
+    // compat tile waves: the longest tiles of the launch order split into splitWays waves (renderKernelWF).
+    // Only where a pixel's sequential chain can outlast the frame's throughput-bound part: long paths
+    // (max_depth > 16; C3, depth 50: 800 -> 766 ms) on kernels without critical-pixel waves, which
+    // take those chains out of the tile waves (C3 with both: 710 ms, critical pixels alone 699 ms).
+    // Short-path frames are throughput-bound and the split's idle lanes cost (C5, depth 16: 548 ->
+    // 553 ms; C2, depth 8: +0.9 %).
+    P.splitWays = std::max(1, std::min(8, envCount("PT_SPLIT_WAYS", 2)));
+    P.splitTiles = (lpt && f->haveOrder && !sample && !cq && kernel != PT_KERNEL_SIMPLE)
+                       ? std::max(0, std::min(P.ntiles, envCount("PT_SPLIT_TILES", max_depth > 16 && !critOn ? 128 : 0))) : 0;
+    if (P.splitWays == 1 || PT_AB_NO_SPLIT) P.splitTiles = 0;   // (a build without the split prologue: grid = tiles)
     P.compatGrid = P.critWaves + P.ntiles + P.splitTiles * (P.splitWays - 1);
     // diagnostic: only the first k waves of the launch order (the longest tiles) -- their chains'
     // latency with the machine otherwise idle; the other pixels are not rendered
