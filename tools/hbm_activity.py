@@ -27,8 +27,8 @@ def sampler():
     while not STOP.is_set():
         t = time.time()
         try:
-            out = subprocess.run(["amd-smi", "metric", "--usage", "--json"], capture_output=True, text=True,
-                                 timeout=10).stdout
+            out = subprocess.run(["amd-smi", "metric", "-g", "0", "--usage", "--json"], capture_output=True,
+                                 text=True, timeout=10).stdout
             SAMPLES.append((t, time.time(), out))
         except Exception as e:   # noqa: BLE001
             SAMPLES.append((t, time.time(), f"error {e}"))
@@ -40,6 +40,8 @@ def umc(text):
         d = json.loads(text)
     except ValueError:
         return None
+    if isinstance(d, dict) and "gpu_data" in d:
+        d = d["gpu_data"]
     d = d[0] if isinstance(d, list) else d
     u = d.get("usage", d)
     v = u.get("umc_activity") or u.get("UMC_ACTIVITY")

@@ -6,6 +6,8 @@
 #     and without the `pipelined` frames, whose overlapping launches last longer than a frame)
 #                                                               -> gpurun_out/$TAG/trace/
 #  3. separate --pmc passes (FETCH_SIZE | WRITE_SIZE | TCC hit/miss | SQ | VALU instructions) on one frame
+#     after one warmup frame of the same kernel (so the counted launch is a steady-state one: sample
+#     mode's first launch on a film also counts every task's rays for the tile order, a 4th atomic)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -13,7 +15,7 @@ TAG=${TAG:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 BENCH_ARGS=${BENCH_ARGS:-}
-PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-compat --no-interactive --no-pipelined}
+PMC_ARGS=${PMC_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-compat --no-interactive --no-pipelined}
 TRACE_ARGS=${TRACE_ARGS:---no-cpu-baseline --no-interactive --no-pipelined}
 step() {  # name, limit, command...
     local name=$1 lim=$2; shift 2
