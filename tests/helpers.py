@@ -158,17 +158,20 @@ def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
     if log_path is None:
         log_path = tempfile.mktemp(suffix=".log")
     t0 = time.perf_counter()
-    # every multi-process log is kept as evidence (PT_TEST_LOG_DIR, default gpurun_out/test_logs/:
-    # the scratch directory a GPU box's results come back in)
+    # Every multi-process log is kept as evidence, written there WHILE the children run (a hang
+    # leaves its ranks' last phases and the watchdog's stack dumps behind even if the whole call is
+    # killed): PT_TEST_LOG_DIR, default gpurun_out/test_logs/ (the directory a GPU box's results
+    # come back in); the test's own log_path then names the file.
     keep = os.environ.get("PT_TEST_LOG_DIR") or os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "test_logs")
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+        log_path = os.path.join(keep, os.path.basename(os.path.dirname(str(log_path))) + "_" +
+                                os.path.basename(str(log_path)))
 
     def kept(text, rc):
-        if keep:
-            os.makedirs(keep, exist_ok=True)
-            name = os.path.basename(os.path.dirname(str(log_path))) + "_" + os.path.basename(str(log_path))
-            with open(os.path.join(keep, name), "w") as f:
-                f.write(text + f"\n[run_logged] rc={rc} wall={time.perf_counter() - t0:.1f} s\n")
+        with open(log_path, "a") as f:
+            f.write(f"\n[run_logged] rc={rc} wall={time.perf_counter() - t0:.1f} s\n")
         return text
 
     with open(log_path, "w+") as log:

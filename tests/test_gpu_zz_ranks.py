@@ -135,8 +135,8 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     """C4 (BASELINE.json configs[3]: the C3 scene at 1920x1080, 4096 spp, row-tiled over 8 GPUs)
     through bench.py's own multi-rank flow: 8 ranks over gloo sharing this one GPU (a rehearsal,
     never a reported number), each rendering its 1/8 of the stripes at the full sample count on the
-    wide tree it built (host SAH, as at N = 1); the gathered, un-permuted PNG equals the 1-rank PNG byte for
-    byte and the rank-0 line reports the whole frame's rays and all eight ranks' figures."""
+    wide tree it built (host SAH, as at N = 1); the gathered, un-permuted PNG equals the 1-rank PNG
+    byte for byte and the rank-0 line reports the whole frame's rays and all eight ranks' figures."""
     import os
     import sys
     from helpers import failure_digest, last_json, read_png, run_logged
@@ -146,11 +146,12 @@ def test_bench_c4_eight_ranks_rehearsal(tmp_path):
     one, eight = str(tmp_path / "one.png"), str(tmp_path / "eight.png")
     rc, log1, _ = run_logged([sys.executable] + common + ["--png", one], 240, cwd=repo, log_path=tmp_path / "r1.log")
     assert rc == 0, failure_digest(log1)
-    # eight processes share one GPU and the box's CPU share here: a rank can reach a collective
-    # minutes after another (start-up, serialised kernels), so the rehearsal's timeouts are wider;
-    # the per-phase watchdog fires before the collective timeout, so a rank stuck in a phase dumps
-    # its own stack (faulthandler) before the others give up on it
-    env = _rank_env(PT_DIST_BACKEND="gloo", PT_DIST_TIMEOUT="300", PT_BENCH_WATCHDOG="240")
+    # eight processes share one GPU and the box's CPU share here, so the rehearsal's collective
+    # timeout is wider than the other tests' (a phase takes a few seconds: 28-46 s for the whole run);
+    # the per-phase watchdog fires before the collective timeout, so a rank stuck in a phase dumps its
+    # own stack (faulthandler) before the others give up on it, and both fire inside the GPU box's
+    # 180-s silence limit; the rank log streams into gpurun_out/test_logs/ as the ranks trace phases
+    env = _rank_env(PT_DIST_BACKEND="gloo", PT_DIST_TIMEOUT="170", PT_BENCH_WATCHDOG="150")
     rc, log8, wall = run_logged(_torchrun(8) + common[:1] + ["--gpus", "8"] + common[1:] + ["--png", eight], 480,
                                 cwd=repo, env=env, log_path=tmp_path / "r8.log")
     assert rc == 0, f"8 ranks failed after {wall:.0f} s\n" + failure_digest(log8)
