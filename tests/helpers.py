@@ -177,7 +177,7 @@ def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
     with open(log_path, "w+") as log:
         # the parent's situation when the child starts: its own GPU state and the box's load
         log.write(f"[run_logged] parent pid {os.getpid()}: loadavg {os.getloadavg()}, "
-                  f"parent GPU context {'yes' if _parent_gpu_state() else 'no'}\n")
+                  f"parent GPU context {'yes' if _parent_gpu_state() else 'no'}{_device_memory()}\n")
         log.flush()
         p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
         try:
@@ -193,6 +193,19 @@ def run_logged(cmd, timeout, cwd=None, env=None, log_path=None):
                                  + kept(log.read(), "timeout")[-4000:])
         log.seek(0)
         return rc, kept(log.read(), rc), time.perf_counter() - t0
+
+
+def _device_memory():
+    """', device memory free / total GiB' when this process's torch has a GPU context, else ''."""
+    import sys
+    t = sys.modules.get("torch")
+    try:
+        if t is not None and t.cuda.is_initialized():
+            free, total = t.cuda.mem_get_info()
+            return f", device memory free {free / 2**30:.1f} of {total / 2**30:.1f} GiB"
+    except Exception:   # noqa: BLE001  (diagnostic only)
+        pass
+    return ""
 
 
 def _parent_gpu_state():

@@ -15,6 +15,21 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _quiet_parent():
+    """Before the multi-process tests: the suite process's own GPU work finished and its freed memory
+    returned (a parent with frames still in flight or large caches is the one difference between these
+    tests late in the suite and alone; each run's log records the parent's state, helpers.run_logged)."""
+    import gc
+    import sys
+    gc.collect()
+    t = sys.modules.get("torch")
+    if t is not None and t.cuda.is_initialized():
+        t.cuda.synchronize()
+        t.cuda.empty_cache()
+    yield
+
+
 def free_port() -> str:
     """A free TCP port on 127.0.0.1 for a torch.distributed.run rendezvous (a fixed port can still be
     held by an earlier run on a shared box)."""
