@@ -487,12 +487,13 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t mbcnt64(uint64_t m) 
 // One compressed 8-wide node (five 16-B words, layout in host/pt_wide8.cpp) against the ray:
 // returns the hit mask, internal children in bits 24 + (slot ^ oct), leaf primitives in bits
 // 0..23 (offsets from the node's primitive base).  Plane distances t = q * (s * inv) + (p - o) *
-// inv; the planes lie a quantum outside the exact boxes, far beyond this arithmetic's rounding,
+// inv; the planes lie at least the tree's smallest quantum 2^emin outside the exact boxes (one
+// node quantum up to round 6), beyond this arithmetic's rounding,
 // and a NaN (0 * inf on an axis the ray is parallel to) only drops that plane: the test never
 // rejects a box the exact slab test (aabb.h:21-34) accepts.
 //
 // The margin holds while |p - o| stays within about 11 times the larger of the scene's extent
-// and its coordinates (the quantum is >= 2^-18 of that, the rounding of the ray's plane distances
+// and its coordinates (the margin is >= 2^-18 of that, the rounding of the ray's plane distances
 // about 2^-21.6 of |p - o|): a ray whose origin lies farther than 8 scene extents from the
 // scene's centre (wideFar) skips this test and is traced in the reference's order instead.
 //
@@ -583,7 +584,7 @@ __device__ __forceinline__ bool zeroAxes(float3 inv) {
 // at all: the ray would enter every child it overlaps in the other two axes -- round 4: 1,000-1,500
 // node visits for C5 rays at the height of the origin).  Here the test itself, on the quantised
 // planes p + q * s: u = (o - p) / s (1 / s a power of two), a child is kept when qlo <= u <= qhi.
-// (The rounding of o - p is far below the planes' one-quantum outward margin, as in wideHits.)
+// (The rounding of o - p is far below the planes' outward margin of >= 2^emin, as in wideHits.)
 // k0 / k1: the children 0-3 / 4-7 byte masks, cleared (bits 5-7) for rejected children.
 __device__ __forceinline__ void zeroAxisKeep(float oc, uint32_t pbits, uint32_t ebyte, uint32_t qlo0, uint32_t qlo1,
                                              uint32_t qhi0, uint32_t qhi1, uint32_t& k0, uint32_t& k1) {
@@ -4785,15 +4786,17 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
     // instanced scenes (no speculative traversal: a lane with primitives waiting cannot visit nodes)
     // take their LEAF steps earlier: LEAF 16 / SHADE 20 (round 5, C5 instanced @128 spp, interleaved
     // median of 3: 131.8 -> 128.8 ms; LEAF 12: 131.8, 8: 135.9, 32: 140.7; SHADE 28 with LEAF 16: 131.4)
-    const bool instSample = wideSample && s->instanced;
+    // (instanced compat takes them too: C5 instanced compat @512 618.6 -> 594.6 ms; 24 / 24: 609.8,
+    // 28 / 28: 646.5)
+    const bool instWide = kernel == PT_KERNEL_WIDE && s->instanced;
     P.leafBatch = (opts && opts->leaf_batch > 0) ? std::min(opts->leaf_batch, 64)
-                                                 : envInt("PT_LEAF_BATCH", instSample ? 16 : (wideSample || wideFlatCompat) ? wideBatch
+                                                 : envInt("PT_LEAF_BATCH", instWide ? 16 : (wideSample || wideFlatCompat) ? wideBatch
                                                                                                        : (sampleRng ? 24 : 20));
     // compat mode: a NODE step with fewer than nodeMin lanes yields to the larger of the waiting
     // LEAF / SHADE groups (C3 compat 1,620 -> 1,517 ms at 8; 4: 1,548, 16: 1,671, 32: 1,989)
     P.nodeMin = std::getenv("PT_NODE_MIN") ? std::atoi(std::getenv("PT_NODE_MIN")) : 8;
     P.shadeBatch = (opts && opts->shade_batch > 0) ? std::min(opts->shade_batch, 64)
-                                                   : envInt("PT_SHADE_BATCH", instSample ? 20 : (wideSample || wideFlatCompat) ? wideBatch
+                                                   : envInt("PT_SHADE_BATCH", instWide ? 20 : (wideSample || wideFlatCompat) ? wideBatch
                                                                                                            : (sampleRng ? 32 : 12));
     if (kernel == PT_KERNEL_SIMPLE) P.leafBatch = 0;
     const size_t ntl = (size_t)std::max(1, P.ntiles);

@@ -387,6 +387,7 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
     }
     int emin = ext > 0.0 ? ceilLog2(ext) - 18 : -100;
     emin = emin < -100 ? -100 : emin;
+    const double minQuantum = ldexp(1.0, emin);
 
     float cmn[8][3], cmx[8][3];
     float nmn[3] = {INFINITY, INFINITY, INFINITY}, nmx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -464,7 +465,8 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
         meta[s >> 2] |= mb << (8 * (s & 3));
     }
     // quantised planes (pt_wide8.cpp): origin below the node box, quantum 2^e with the node
-    // extent <= 251 quanta, child planes rounded outward by one more quantum
+    // extent <= 251 quanta, child planes rounded outward by the smallest quantum 2^emin (the margin the
+    // traversal's rounding bound needs; pt_wide8.cpp)
     uint32_t R[20];
     uint32_t exps = 0;
     for (int a = 0; a < 3; a++) {
@@ -486,8 +488,8 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
                 const int j = childIn[sl];
                 uint32_t l8 = 255u, h8 = 0u;
                 if (j >= 0) {
-                    const double qlo = floor(((double)cmn[j][a] - (double)p) / s) - 1.0;
-                    const double qhi = ceil(((double)cmx[j][a] - (double)p) / s) + 1.0;
+                    const double qlo = floor(((double)cmn[j][a] - minQuantum - (double)p) / s);
+                    const double qhi = ceil(((double)cmx[j][a] + minQuantum - (double)p) / s);
                     if (!(qlo >= 0.0) || !(qhi <= 255.0)) {
                         ok = false;
                         break;

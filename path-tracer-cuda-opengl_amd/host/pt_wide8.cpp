@@ -12,9 +12,10 @@
 //   [6..7]  meta byte per slot: 0 = empty; internal 0b001_11000 | j; leaf (unary count << 5) | offset
 //   [8..11] qlo_x[0..3], qlo_x[4..7], qhi_x[0..3], qhi_x[4..7]     (8-bit planes, byte j = slot j)
 //   [12..15] the same for y, [16..19] for z
-// A child box is [p + qlo * s, p + qhi * s] per axis, rounded OUTWARD by at least one quantum
-// beyond the exact box, so a slab test on it (with any fp32 rounding of the ray arithmetic) is
-// conservative: it never rejects a box the exact test accepts.
+// A child box is [p + qlo * s, p + qhi * s] per axis, rounded OUTWARD by at least the tree's
+// smallest quantum 2^emin (2^-18 of the scene's extent and coordinates) beyond the exact box, so a
+// slab test on it (with any fp32 rounding of the ray arithmetic) is conservative: it never rejects
+// a box the exact test accepts.
 //
 // Slots are ordered per ray octant: slot j holds the child nearest along the octant direction j
 // (bit a of j set = negative direction on axis a).  A ray of octant o visits internal children
@@ -374,6 +375,11 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
     int emin = ext > 0.0 ? (int)std::ceil(std::log2(ext)) - 18 : -100;
     emin = std::max(emin, -100);
 
+    // outward margin of the child planes: PT_WIDE_MARGIN=0 one quantum of the node (the round-1..6
+    // rule), otherwise the smallest quantum 2^emin (what the rounding bound above needs)
+    const char* mg = std::getenv("PT_WIDE_MARGIN");
+    const bool nodeMargin = mg && *mg == '0';
+    const double minQuantum = std::ldexp(1.0, emin);
     const char* sl = std::getenv("PT_WIDE_SPLIT_LEAVES");
     const bool splitLeaves = !(sl && *sl == '0');
     struct Work { int32_t bnode; int64_t slot; int depth; };
@@ -486,7 +492,9 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
             }
         }
         // quantised planes: origin one quantum below the node box, quantum s = 2^e with the
-        // node extent <= 251 s, child planes rounded outward by one more quantum
+        // node extent <= 251 s, child planes rounded outward by the margin m (the smallest quantum:
+        // round 6, C3 @256 spp 134.8 -> 131.2 ms, C5 @64 65.3 -> 62.2, C2 @1024 115.9 -> 114.4, the
+        // same frames; 2.1 % fewer node visits, 1.4 % fewer primitive tests)
         uint32_t* R = &out.nodes[(size_t)w.slot * kW8NodeDwords];
         uint8_t qlo[3][8], qhi[3][8];
         uint32_t exps = 0;
@@ -500,6 +508,7 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
                     return false;
                 }
                 const double s = std::ldexp(1.0, e);
+                const double m = nodeMargin ? s : minQuantum;
                 float p = (float)(lo - s);
                 if ((double)p > lo - s) p = std::nextafter(p, -INFINITY);
                 bool ok = true;
@@ -507,8 +516,8 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
                     const int c = childIn[j];
                     if (c < 0) { qlo[a][j] = 255; qhi[a][j] = 0; continue; }
                     const BBox& b = B.nodes[ch[c]].box;
-                    const double ql = std::floor(((double)b.mn[a] - (double)p) / s) - 1.0;
-                    const double qh = std::ceil(((double)b.mx[a] - (double)p) / s) + 1.0;
+                    const double ql = std::floor(((double)b.mn[a] - m - (double)p) / s);
+                    const double qh = std::ceil(((double)b.mx[a] + m - (double)p) / s);
                     if (!(ql >= 0.0) || !(qh <= 255.0)) { ok = false; break; }
                     qlo[a][j] = (uint8_t)ql;
                     qhi[a][j] = (uint8_t)qh;

@@ -14,6 +14,7 @@ import csv
 import json
 import os
 import shutil
+import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -44,8 +45,10 @@ def main(tag):
     write = render_launches(os.path.join(dst, "pmc_write.csv"), "WRITE_SIZE")
     wf_fetch = [v for k, v in fetch if "renderKernelWF" in k] or [fetch[-1][1]]
     wf_write = [v for k, v in write if "renderKernelWF" in k] or [write[-1][1]]
-    fetch_b = 2.0 * wf_fetch[-1] * 1024.0
-    write_b = wf_write[-1] * 1024.0
+    # the median launch: a run of several frames holds a cost-measuring launch every few frames
+    # (the tile order's refresh: one more atomic per task), the steady-state launches are the rest
+    fetch_b = 2.0 * steady(wf_fetch) * 1024.0
+    write_b = steady(wf_write) * 1024.0
     cfg = bench["config"]
     out = {
         "workload": cfg["workload"], "spp": cfg["spp"], "rng": cfg["rng"],
@@ -65,8 +68,8 @@ def main(tag):
         hit = [v for k, v in render_launches(tcc_csv, "TCC_HIT_sum") if "renderKernelWF" in k]
         miss = [v for k, v in render_launches(tcc_csv, "TCC_MISS_sum") if "renderKernelWF" in k]
         if hit and miss:
-            out["tcc_hit"], out["tcc_miss"] = hit[-1], miss[-1]
-            out["tcc_hit_rate"] = hit[-1] / max(1.0, hit[-1] + miss[-1])
+            out["tcc_hit"], out["tcc_miss"] = steady(hit), steady(miss)
+            out["tcc_hit_rate"] = out["tcc_hit"] / max(1.0, out["tcc_hit"] + out["tcc_miss"])
     store("traffic", out)
     print(json.dumps(out, indent=1))
     # VALU wave-instructions per launch of the timed (wavefront) render kernel: the wide kernel's
@@ -76,11 +79,16 @@ def main(tag):
         valu = [v for k, v in render_launches(valu_csv, "SQ_INSTS_VALU") if "renderKernelWF" in k]
         if valu:
             v = {key: out[key] for key in ("workload", "spp", "rng", "kernel")}
-            v["valu_wave_instructions_per_launch"] = valu[-1]
+            v["valu_wave_instructions_per_launch"] = steady(valu)
             v["source"] = f"profiles/{tag}/pmc_valu.csv (rocprofv3 --pmc SQ_INSTS_VALU, one frame)"
             v["build_id"] = bench["build_id"]
             store("valu", v)
             print(json.dumps(v, indent=1))
+
+
+def steady(vals):
+    """The median of a run's wavefront render launches (the single launch of a one-frame run)."""
+    return float(statistics.median(vals))
 
 
 def store(name, entry):

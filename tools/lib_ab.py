@@ -22,6 +22,7 @@ def main():
         libs.append((parts[0], parts[1], parts[2] if len(parts) > 2 else "0", parts[3] if len(parts) > 3 else ""))
     times = {n: [] for n, _, _, _ in libs}
     digests = {}
+    work = {}
     for r in range(rounds):
         for name, lib, chunk, envs in libs:
             env = dict(os.environ, PT_LIB=os.path.join(REPO, lib), REPEAT=os.environ.get("REPEAT", "2"))
@@ -34,10 +35,11 @@ def main():
             d = json.loads(out.stdout.strip().splitlines()[-1])
             times[name].append(d["kernel_ms"])
             digests[name] = d["image"]
+            work[name] = {"node_visits": d.get("node_visits"), "tri_tests": d.get("tri_tests")}
             print(f"round {r} {name}: {d['kernel_ms']:.2f} ms", flush=True)
     for name, _, _, _ in libs:
         print(json.dumps({"build": name, "median_ms": statistics.median(times[name]), "all": times[name],
-                          "image": digests[name]}))
+                          "image": digests[name], **work[name]}))
 
 
 if __name__ == "__main__":
