@@ -3,11 +3,14 @@
 // never uses it).  Reads objects and rays, builds the binary LBVH with the oracle (oracle/), the
 // reference ranks and the wide tree exactly as libpt does, then
 //   1. checks the tree: every primitive once, child boxes contain the exact primitive boxes
-//      (outward-quantised planes), node/primitive encodings in range;
+//      with at least the tree's smallest quantum 2^emin to spare on every side (the outward margin
+//      the traversal's rounding bound needs, pt_device.hip wideHits), node/primitive encodings in
+//      range;
 //   2. traces every ray through a scalar restatement of renderKernelWF<.., WIDE>'s NODE / LEAF
 //      steps (nearest-first slots, conservative quantised slab test, (t, tie rank) minimum,
 //      the reference's leaf box test, the redo rule) and writes {leaf k or -1, t, redo} per ray.
 // usage: wide8_check objects.bin rays.bin out.bin
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -223,7 +226,20 @@ int main(int argc, char** argv) {
     }
     P = w.prims.data();
     N = w.nodes.data();
-    // 1. structure
+    // 1. structure.  The smallest quantum, as the builder takes it: 2^-18 of the larger of the
+    // scene's extent and coordinates (rounded up to a power of two)
+    double ext = 0.0;
+    {
+        double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int64_t k = 0; k < n; k++)
+            for (int a = 0; a < 3; a++) {
+                mn[a] = std::fmin(mn[a], (double)boxes[(size_t)k * 6 + a]);
+                mx[a] = std::fmax(mx[a], (double)boxes[(size_t)k * 6 + 3 + a]);
+            }
+        for (int a = 0; a < 3; a++) ext = std::fmax(ext, std::fmax(std::fmax(std::fabs(mn[a]), std::fabs(mx[a])), mx[a] - mn[a]));
+    }
+    const int emin = ext > 0.0 ? std::max(-100, (int)std::ceil(std::log2(ext)) - 18) : -100;
+    const double minQuantum = std::ldexp(1.0, emin);
     std::vector<int> seen((size_t)n, 0);
     std::vector<int> kOfRank((size_t)n, -1);
     for (int64_t k = 0; k < n; k++) kOfRank[rank[k]] = (int)k;
@@ -255,7 +271,8 @@ int main(int argc, char** argv) {
             auto contains = [&](int64_t prim) {
                 const int64_t k = kOfRank[w.prims[(size_t)prim * 12 + 3]];
                 for (int a = 0; a < 3; a++)
-                    if (!(lo[a] < (double)boxes[(size_t)k * 6 + a] && hi[a] > (double)boxes[(size_t)k * 6 + 3 + a]))
+                    if (!(lo[a] <= (double)boxes[(size_t)k * 6 + a] - minQuantum &&
+                          hi[a] >= (double)boxes[(size_t)k * 6 + 3 + a] + minQuantum))
                         return false;
                 return true;
             };
