@@ -46,7 +46,12 @@ def summary(t, top=12):
     order = np.argsort(-dur * ok)
     longest = [{"wave": int(i), "tile": int(t[i, 2] & 0xffffffff), "start_ms": round(float(s[i]), 2),
                 "dur_ms": round(float(dur[i]), 2)} for i in order[:top] if ok[i]]
-    return {"waves": int(ok.sum()), "span_ms": float(e[ok].max()),
+    last = np.argsort(-e * ok)
+    latest = [{"wave": int(i), "tile": int(t[i, 2] & 0xffffffff), "start_ms": round(float(s[i]), 2),
+               "dur_ms": round(float(dur[i]), 2)} for i in last[:top] if ok[i]]
+    # how long the machine runs below full occupancy: waves still running at the p-th end-time
+    return {"waves": int(ok.sum()), "span_ms": float(e[ok].max()), "latest": latest,
+            "start_pct_ms": {str(q): round(float(np.percentile(s[ok], q)), 1) for q in (50, 90, 99, 100)},
             "end_pct_ms": {str(q): round(float(np.percentile(e[ok], q)), 1) for q in (50, 90, 99, 99.9, 100)},
             "longest": longest}
 
