@@ -617,9 +617,13 @@ __device__ __forceinline__ uint32_t wideHitsInst(uint4 n0, uint4 n1, uint4 n2, u
 
 // The ray origin lies farther than 8 scene extents from the scene's centre on some axis, beyond
 // the distance the wide boxes' margin covers (wideHits): the query runs in the reference's order.
+#ifndef PT_WIDE_FAR_EXT
+#define PT_WIDE_FAR_EXT 8.0f   // with the builders' PT_WIDE_EMIN_SHIFT 18 (host/pt_wide8.cpp)
+#endif
+constexpr float kWideFarExt = PT_WIDE_FAR_EXT;
 __device__ __forceinline__ bool wideFar(float cx, float cy, float cz, float ext, float3 o) {
     const float m = fmaxf(fmaxf(fabsf(o.x - cx), fabsf(o.y - cy)), fabsf(o.z - cz));
-    return !(m <= 8.0f * ext);   // (NaN: far)
+    return !(m <= kWideFarExt * ext);   // (NaN: far)
 }
 __device__ __forceinline__ bool wideFar(const DevScene& S, float3 o) { return wideFar(S.cx, S.cy, S.cz, S.ext, o); }
 // Instanced scenes draw the line at 2 world extents: their mesh trees are quantised for origins
@@ -4765,7 +4769,7 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         for (int a = 0; a < 3; a++)
             m = std::max(m, std::fabs((double)cam->origin[a] - (double)s->sceneCE[a]) +
                                 (double)cam->lens_radius * (std::fabs((double)cam->right[a]) + std::fabs((double)cam->up[a])));
-        P.camFar = !(m <= (s->wideSource == 3 ? (double)kInstFarExt : 8.0) * (double)s->sceneCE[3]) ? 1 : 0;
+        P.camFar = !(m <= (s->wideSource == 3 ? (double)kInstFarExt : (double)kWideFarExt) * (double)s->sceneCE[3]) ? 1 : 0;
     }
     // Defaults swept on C3 (tools/ab_env.py): sample mode is throughput-bound and prefers full
     // LEAF / SHADE steps.  Compat mode on the binary tree is bound by its slowest pixels' sequential

@@ -25,6 +25,10 @@
 #include "pt_wide8.hpp"
 #include "pt_wide_dev.hpp"
 
+#ifndef PT_WIDE_EMIN_SHIFT
+#define PT_WIDE_EMIN_SHIFT 18   // the smallest plane quantum, as host/pt_wide8.cpp
+#endif
+
 namespace pt {
 namespace {
 
@@ -385,7 +389,7 @@ __global__ void wideWriteKernel(Tree T, const uint2* __restrict__ items, int m, 
         for (int a = 0; a < 3; a++)
             ext = fmax(ext, fmax(fabs((double)l[a]), fmax(fabs((double)h[a]), (double)h[a] - (double)l[a])));
     }
-    int emin = ext > 0.0 ? ceilLog2(ext) - 18 : -100;
+    int emin = ext > 0.0 ? ceilLog2(ext) - PT_WIDE_EMIN_SHIFT : -100;
     emin = emin < -100 ? -100 : emin;
     const double minQuantum = ldexp(1.0, emin);
 

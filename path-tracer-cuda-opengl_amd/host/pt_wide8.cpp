@@ -58,6 +58,11 @@ struct BNode {
 };
 
 constexpr int kBins = 32;
+// The smallest plane quantum is 2^-PT_WIDE_EMIN_SHIFT of the scene's extent and coordinates; the
+// traversal's far-origin line (pt_device.hip PT_WIDE_FAR_EXT) must match it (A/B knobs, one pair).
+#ifndef PT_WIDE_EMIN_SHIFT
+#define PT_WIDE_EMIN_SHIFT 18
+#endif
 constexpr double kPrimCost = 1.0;
 
 // Build parameters (tuning knobs, PT_WIDE_MAX_LEAF / PT_WIDE_TRAV_COST): at most kMaxLeaf <= 3
@@ -372,7 +377,7 @@ bool buildWide8Leaf(const uint32_t* prims, const float* boxes, const uint32_t* r
     for (int a = 0; a < 3; a++)
         ext = std::max({ext, std::fabs((double)rootBox.mn[a]), std::fabs((double)rootBox.mx[a]),
                         (double)rootBox.mx[a] - (double)rootBox.mn[a]});
-    int emin = ext > 0.0 ? (int)std::ceil(std::log2(ext)) - 18 : -100;
+    int emin = ext > 0.0 ? (int)std::ceil(std::log2(ext)) - PT_WIDE_EMIN_SHIFT : -100;
     emin = std::max(emin, -100);
 
     // outward margin of the child planes: PT_WIDE_MARGIN=0 one quantum of the node (the round-1..6
