@@ -1261,6 +1261,14 @@ constexpr int kLeafQ = PT_LEAF_QUEUE;
 #define PT_TASK_POOL 64
 #endif
 constexpr int kTaskPool = PT_TASK_POOL;   // sample mode: tasks a wave reserves per atomic
+// Experiment (off): XCD-local task pools.  The tile slots are dealt to 8 counters (slot % 8), a
+// wave drains the counter of its XCD (blockIdx % 8: workgroups are dispatched to the XCDs round
+// robin) and then the others in turn, so each XCD's L2 sees the rays of an eighth of the tiles
+// in flight.  Exact by construction: the image does not depend on which lane runs a task.
+#ifndef PT_XCD_POOLS
+#define PT_XCD_POOLS 0
+#endif
+static_assert(!PT_XCD_POOLS || PT_TASK_POOL == 64, "XCD pools hand out whole (tile, block) groups");
 #ifndef PT_TASK_GROUPS
 #define PT_TASK_GROUPS 0   // wide sample kernels: tasks of several summation blocks (LDS partials; measured slower)
 #endif
@@ -1604,6 +1612,38 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
     // Task t = (tile slot t / 64 / nblocks in launch order, block (t / 64) % nblocks, pixel
     // t % 64 of the 8x8 tile); tasks off the frame edge are skipped.  Sets `got` for lanes
     // that received a task; lanes that find the counter exhausted stop asking.
+#if PT_XCD_POOLS
+    // counter x holds the groups of tile slots x, x + 8, ...: local group lg = slot / 8 * ngroups +
+    // block.  A wave tries its own XCD's counter first, then the others in turn (no state kept: an
+    // exhausted counter costs a wave one more atomic per refill; the host keeps the overshoot far
+    // from wrapping, ntasks < 2^28); all eight empty: poolBase = ntasks
+#define PT_POOL_REFILL(grab, leader)                                                                \
+    do {                                                                                          \
+        uint32_t gb_ = Q_.ntasks;                                                                 \
+        for (uint32_t i_ = 0; i_ < 8u; i_++) {                                                    \
+            const uint32_t x_ = (blockIdx.x + i_) & 7u;                                           \
+            uint32_t lb_ = 0;                                                                     \
+            if (lane == (leader)) lb_ = atomicAdd(Q_.taskCounter + x_, (grab));                   \
+            lb_ = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)lb_, (leader)));           \
+            const uint32_t lg_ = lb_ >> 6, ng_ = (uint32_t)Q_.ngroups;                            \
+            const uint32_t nt_ = (uint32_t)Q_.ntiles;                                             \
+            const uint32_t nLocal_ = x_ < nt_ ? (nt_ - x_ + 7u) >> 3 : 0u;                        \
+            if (lg_ < nLocal_ * ng_) {                                                            \
+                const uint32_t q_ = lg_ / ng_, blk_ = lg_ - q_ * ng_;                              \
+                gb_ = ((8u * q_ + x_) * ng_ + blk_) << 6;                                         \
+                break;                                                                            \
+            }                                                                                     \
+        }                                                                                         \
+        poolBase = gb_;                                                                           \
+    } while (0)
+#else
+#define PT_POOL_REFILL(grab, leader)                                                                \
+    do {                                                                                          \
+        uint32_t b_ = 0;                                                                          \
+        if (lane == (leader)) b_ = atomicAdd(Q_.taskCounter, (grab));                             \
+        poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, (leader)));           \
+    } while (0)
+#endif
 #define PT_TAKE_TASKS(got)                                                                          \
     do {                                                                                          \
         const auto& Q_ = *kargs();                                                                \
@@ -1615,9 +1655,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWavesPer
                 /* always a full pool: = one (tile, block) group, one task per lane; smaller    \
                    grabs near the end measured slower (1/8 share: 150-158 vs 145 ms) */          \
                 const uint32_t grab_ = (uint32_t)kTaskPool;                                       \
-                uint32_t b_ = 0;                                                                  \
-                if (lane == leader_) b_ = atomicAdd(Q_.taskCounter, grab_);                        \
-                poolBase = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)b_, leader_));    \
+                PT_POOL_REFILL(grab_, leader_);                                                   \
                 poolLeft = grab_;                                                                 \
             }                                                                                     \
             /* wave-uniform: the taken tasks span task groups (tile slot, blocks) g0 and g0 + 1 */ \
@@ -4907,8 +4945,14 @@ int pt_render_ex(pt_scene* s, pt_film* f, const pt_camera* cam, int spp, int max
         if (ntasks >= (1ull << 32) - 4096)
             return fail(PT_ERR_INVALID, "sample mode: too many (pixel, block) tasks; raise the block size (chunk)");
         P.ntasks = (uint32_t)ntasks;
+        if (PT_XCD_POOLS && ntasks >= (1ull << 28))
+            return fail(PT_ERR_INVALID, "sample mode with XCD pools: too many tasks; raise the block size (chunk)");
         if (!f->taskCounter.p && (rc = devAlloc(f->taskCounter, 64))) return rc;
+#if PT_XCD_POOLS
+        HIP_TRY(hipMemsetAsync(f->taskCounter.p, 0, 32, st));   // the eight XCD counters
+#else
         HIP_TRY(hipMemsetAsync(f->taskCounter.p, 0, 4, st));
+#endif
         P.taskCounter = f->taskCounter.as<unsigned>();
         int perCU = 0;
         if ((rc = perCUFor(perCU))) return rc;
