@@ -170,6 +170,32 @@ def test_wide_frame_equals_reference_order_frame(pt, gpu, wb, cfg, w, h, spp):
         assert out[pt.KERNEL_WIDE][1].rays == out[pt.KERNEL_WAVEFRONT][1].rays
 
 
+@pytest.mark.parametrize("cfg,w,h,spp", [("bunny_cornell", 192, 108, 8), ("bunny_field", 160, 90, 2)])
+def test_plane_margin_changes_work_not_frames(pt, gpu, monkeypatch, cfg, w, h, spp):
+    """Round 6 (DESIGN §5 "Plane margin"): the host tree's child planes lie the tree's smallest
+    quantum outside the exact boxes instead of one node quantum (PT_WIDE_MARGIN=0).  The margin is
+    a pure performance choice: both RNG modes' frames stay bit-identical (and equal to the binary
+    reference-order kernel's) while the tighter boxes visit fewer nodes and test fewer primitives."""
+    p = pt.Preset(cfg, w, h)
+    work = {}
+    for margin in ("0", "1"):
+        monkeypatch.setenv("PT_WIDE_MARGIN", margin)
+        s = pt.Scene(p.objects, p.materials, device=gpu, flags=pt.PT_BVH_ORIGIN_BOUNDS)
+        for rng in (pt.RNG_COMPAT, pt.RNG_SAMPLE):
+            f = pt.Film(w, h, 7, device=gpu)
+            work[margin, rng] = pt.render(s, f, p.camera, spp, p.max_depth, kernel=pt.KERNEL_WIDE, rng=rng)
+        assert s.wide_info()["source"] == 1
+    ref = pt.Scene(p.objects, p.materials, device=gpu, flags=pt.PT_BVH_ORIGIN_BOUNDS)
+    for rng in (pt.RNG_COMPAT, pt.RNG_SAMPLE):
+        (img0, st0), (img1, st1) = work["0", rng], work["1", rng]
+        base = pt.render(ref, pt.Film(w, h, 7, device=gpu), p.camera, spp, p.max_depth, kernel=pt.KERNEL_WAVEFRONT,
+                         rng=rng)[0]
+        np.testing.assert_array_equal(bits(img1), bits(img0))
+        np.testing.assert_array_equal(bits(img1), bits(base))
+        assert st1.rays == st0.rays
+        assert st1.node_visits < st0.node_visits and st1.tri_tests <= st0.tri_tests, (rng, st0, st1)
+
+
 def test_wide_large_soup_trace_and_render(pt, orc, gpu, wb):
     """200,000 random triangles and spheres: hit records against the oracle, and a frame against
     the reference-order kernel."""
